@@ -1,0 +1,239 @@
+"""Benchmark: SGLD steps/s of the tensor-GP sampler on kin40k (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--chains C] ...
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Workload (BASELINE config 3/4): kin40k — Ntrain = 10 000 rows (the reference's
+own kin40k_train files, whitened as kin40kExperiment.jl:25-37), D = 8, n = 500 random
+features per dimension, rank r = 5, Q = 200, minibatch m = 50, εw = 1e-4, εU = 1e-7,
+σ² = 0.0476, ℓ/σ_RBF of kin40kExperiment.jl:22-23.  phi (320 MB) is built on the device by
+the feature kernel and stays resident in HBM.  Each GPU runs C independent posterior chains
+(seeds differ, phi shared — BASELINE config 4 has one chain per GPU; C chains per GPU is the
+same thing with the GPU filled).  A "step" is one SGLD step of one chain over one minibatch;
+value = chain-steps/s summed over all chains and GPUs (weak scaling: work per GPU fixed).
+After the timed region each GPU predicts the 30 000 test rows with its chains' final
+samples; ranks all-reduce (RCCL) the predictive mean and rank 0 reports the ensemble RMSE.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector/matrix peak (spec)
+
+
+def kin40k(D):
+    d = np.load(os.path.join(ROOT, "tests", "golden", "kin40k.npz"))
+    Xtr, ytr, Xte, yte = d["Xtrain"], d["ytrain"].ravel(), d["Xtest"], d["ytest"].ravel()
+    mu, sd = Xtr.mean(axis=0), Xtr.std(axis=0, ddof=1)
+    ymu, ysd = ytr.mean(), ytr.std(ddof=1)
+    Xtr = (Xtr - mu) / sd                       # datawhitening (GPT_SGLD.jl:62-67)
+    Xte = (Xte - mu) / sd                       # kin40kExperiment.jl:36
+    return Xtr[:, :D], (ytr - ymu) / ysd, Xte[:, :D], (yte - ymu) / ysd, ysd
+
+
+def algorithmic_bytes_per_step(n, D, B, r, Q):
+    """8·(n·D·B + B + 2·n·r·D + 2·Q) + 4·Q·D bytes per SGLD step."""
+    return 8 * (n * D * B + B + 2 * n * r * D + 2 * Q) + 4 * Q * D
+
+
+def algorithmic_flops_per_step(n, D, B, r, Q):
+    return 4 * n * r * D * B + 3 * Q * D * B + 4 * Q * B + D * (14 * n * r * r + 2 * 30 * (2 * r) ** 3)
+
+
+def cpu_baseline(phi_np, y_np, I, args, seconds):
+    """Oracle (numpy fp64 restatement, single BLAS thread) on the same workload, bounded."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:                                   # pragma: no cover
+        threadpool_limits = None
+    from oracle import gpt_sgld_ref as R
+    ctx = threadpool_limits(limits=1) if threadpool_limits else None
+    try:
+        if ctx:
+            ctx.__enter__()
+        kw = dict(store_every=10 ** 9)
+        steps = 5
+        while True:
+            t0 = time.perf_counter()
+            R.GPTregression(phi_np, y_np, args.signal_var, I, args.r, args.Q, args.m, args.epsw,
+                            args.epsU, 0, 1, 1, max_steps=steps, **kw)
+            dt = time.perf_counter() - t0
+            if dt >= seconds or steps >= 200:
+                break
+            steps = min(200, max(steps + 1, int(steps * seconds / max(dt, 1e-3) * 1.05)))
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+    return dict(value=steps / dt, unit="SGLD steps/s (1 chain)", cores=1, kind="port",
+                sample="oracle/gpt_sgld_ref.py GPTregression, %d steps of the kin40k config "
+                       "(n=%d, D=%d, r=%d, Q=%d, m=%d), numpy fp64, 1 BLAS thread, %.1f s incl. init"
+                       % (steps, args.n, args.D, args.r, args.Q, args.m, dt))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--chains", type=int, default=28, help="independent chains per GPU")
+    ap.add_argument("--n", type=int, default=500)
+    ap.add_argument("--D", type=int, default=8)
+    ap.add_argument("--r", type=int, default=5)
+    ap.add_argument("--Q", type=int, default=200)
+    ap.add_argument("--m", type=int, default=50)
+    ap.add_argument("--epsw", type=float, default=1e-4)
+    ap.add_argument("--epsU", type=float, default=1e-7)
+    ap.add_argument("--signal_var", type=float, default=0.0476)
+    ap.add_argument("--kernel-steps", type=int, default=100, help="steps of the event-timed pass")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--single-chain", action="store_true", help="also time C=1 latency")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from gpt_amd import GPT_SGLD as G
+    from gpt_amd.session import SGLDSession, feature_device, pred_device
+
+    n, D, r, Q, m = args.n, args.D, args.r, args.Q, args.m
+    Xtr, ytr, Xte, yte, ysd = kin40k(D)
+    N, Nte = Xtr.shape[0], Xte.shape[0]
+    ls = np.array([2.5242, 2.3376, 1.3630, 1.4949, 1.6022, 1.1366, 1.1964, 1.7028])[:D]
+    sigma_rbf = 1.0420
+    scale = math.sqrt(n / Q ** (1.0 / D))                 # kin40kExperiment.jl:45
+    I = G.samplenz(r, D, Q, 17)                           # :44 (seed 17)
+    Z, b = G.feature_inputs(n, D, 17)                     # Gen-C seeded feature inputs
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    phi_tr = feature_device(tt(Xtr.T), tt(ls), sigma_rbf, scale, tt(Z.T), tt(b.T))
+    phi_te = feature_device(tt(Xte.T), tt(ls), sigma_rbf, scale, tt(Z.T), tt(b.T))
+    y_tr = tt(ytr)
+    torch.cuda.synchronize()
+
+    nb = -(-N // m)
+    C = args.chains
+    need = args.warmup + args.steps + args.kernel_steps
+    epochs = -(-need // nb) + 1
+    seeds = [1000 * rank + c + 1 for c in range(C)]
+    sess = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0, epochs,
+                       seeds, store_every=nb, store=True)
+    sess.run(args.warmup)
+    sess.sync()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sess.run(args.steps)
+    sess.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dt = float(tmax.item())
+    total_steps = C * args.steps * world
+    value = total_steps / dt
+    ms_per_step = 1000.0 * dt / args.steps
+
+    # per-launch kernel time (hipEvents around each step-kernel launch on the session stream)
+    k_us = sess.time_steps(args.kernel_steps)
+    B = m
+    bytes_launch = C * algorithmic_bytes_per_step(n, D, B, r, Q)
+    achieved = bytes_launch / (k_us * 1e-6) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            pm = json.load(open(args.pmc))
+            key = "C%d_n%d_D%d_r%d_Q%d_m%d" % (C, n, D, r, Q, m)
+            traffic = pm.get(key, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    # test prediction with each chain's final state, ensemble mean over chains and ranks
+    I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
+    npred = min(C, 8)
+    fsum = torch.zeros(Nte, dtype=torch.float64, device=dev)
+    fh = torch.empty(Nte, dtype=torch.float64, device=dev)
+    for c in range(npred):
+        wp, Up, _, _, _ = sess.device_state(c)
+        pred_device(wp, Up, I0, phi_te, n, D, Nte, r, Q, 1, fh)
+        fsum += fh
+    torch.cuda.synchronize()
+    ta = time.perf_counter()
+    if world > 1:
+        dist.all_reduce(fsum)                         # RCCL: predictive-mean gather (config 4)
+        torch.cuda.synchronize()
+    allreduce_ms = 1000.0 * (time.perf_counter() - ta)
+    fmean = (fsum / (npred * world)).cpu().numpy()
+    rmse = float(ysd * np.linalg.norm(yte - fmean) / math.sqrt(Nte))
+
+    single = None
+    if args.single_chain and rank == 0:
+        s1 = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0,
+                         epochs, [7], store_every=nb, store=False)
+        s1.run(args.warmup); s1.sync()
+        t1 = time.perf_counter(); s1.run(args.steps); s1.sync()
+        single = args.steps / (time.perf_counter() - t1)
+        s1.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        phi_np = np.asfortranarray(phi_tr.cpu().numpy().transpose(2, 1, 0))
+        cpu = cpu_baseline(phi_np, ytr, I, args, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": "SGLD steps/sec (kin40k, n_feat=500/dim, r=5)",
+            "value": value,
+            "unit": "chain-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "kin40k reference files (tests/golden/kin40k.npz), whitened; features on device",
+            "config": {"workload": "kin40k tensor-GP SGLD (GPTregression)", "Ntrain": N, "Ntest": Nte,
+                       "D": D, "n_features": n, "r": r, "Q": Q, "minibatch": m,
+                       "chains_per_gpu": C, "epsw": args.epsw, "epsU": args.epsU,
+                       "signal_var": args.signal_var, "parallelism": "chains%dx%d" % (C, world)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "sgld_step_kernel<5>", "kernel_us": k_us,
+                         "algorithmic_bytes_per_launch": bytes_launch},
+            "cpu_baseline": cpu,
+            "test_rmse": rmse,
+            "test_rmse_note": "ensemble of %d chains x %d ranks after %d steps/chain (%.1f epochs)"
+                              % (npred, world, args.warmup + args.steps, (args.warmup + args.steps) / nb),
+            "allreduce_ms": allreduce_ms,
+            "single_chain_steps_per_s": single,
+        }
+        print(json.dumps(out))
+    sess.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,252 @@
+"""Python mirror of the reference's ``GPT_SGLD`` / ``GPT_SGLD_p`` Julia module API, running on
+libgptsgld.so (HIP, gfx950).
+
+Same function names, argument meaning, return values and error behaviour as the reference:
+
+    feature(X, length_scale, sigma_RBF, phi_scale, Z, b)      GPT_SGLD.jl:71    (Gen D)
+    feature(X, n, length_scale, sigma_RBF, seed, scale)       kin40kExperiment.jl:71 (Gen C)
+    feature(X, n, length_scale, seed)                         GPT_SGLD_p.jl:40  (Gen A)
+    featureNotensor(X, length_scale, sigma_RBF, Z, b)         GPT_SGLD.jl:109   (Gen D)
+    featureNotensor(X, n, length_scale, sigma_RBF, seed)      PowerPlantNoTensorExperiment.jl:32
+    samplenz(r, D, Q, seed)                                   GPT_SGLD_p.jl:57
+    GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch[, param_seed];
+                  langevin, stiefel)                          GPT_SGLD.jl:345
+    GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch)  GPT_SGLD_p.jl:146
+    pred(w, U, I, phitest)                                    GPT_SGLD.jl:233
+    RMSE(w_store, U_store, I, phitest, ytest)                 GPT_SGLD_p.jl:124
+    GPNT_SGLD(phi, y, signal_var, sigma_theta, m, eps_theta, decay_rate, burnin, maxepoch,
+              param_seed)                                     GPT_SGLD.jl:809
+    datawhitening(X), proj, geod are not on the device path (host prep / inside the kernel).
+
+Arrays follow Julia's column-major layout: ``phi`` is (n, D, N) Fortran-ordered, ``U`` is
+(n, r, D), ``I`` is (Q, D) Int32 1-based.  Like the reference, a NaN in the geodesic prints
+"Get NaN when moving along Geodesic. Try smaller epsU" and returns all-zero stores
+(GPT_SGLD.jl:23-26,422-424); bad dimensions raise (the reference's ``error(...)``).
+
+RNG: Julia's MersenneTwister stream is replaced by the framework's Philox contract
+(oracle/philox.py documents it); seeds play the same role (``srand(param_seed)``).
+"""
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import C, P_D, P_I32, SGLDConfig, check, lib
+
+
+def _f64(a):
+    return np.asfortranarray(np.asarray(a, dtype=np.float64))
+
+
+def _ptr(a, t=P_D):
+    return a.ctypes.data_as(t)
+
+
+# ------------------------------------------------------------------ data preparation (host)
+def datawhitening(X):
+    """GPT_SGLD.jl:62-67 — per-column (x - mean)/std, n-1 denominator (host-side data prep)."""
+    X = np.array(X, dtype=np.float64, copy=True)
+    if X.ndim == 1:
+        return (X - X.mean()) / X.std(ddof=1)
+    return (X - X.mean(axis=0)) / X.std(axis=0, ddof=1)
+
+
+# ------------------------------------------------------------------ features
+def feature_inputs(n, D, seed):
+    """Seeded ``Z = randn(n,D)``, ``b = 2π·rand(n,D)`` (Generation-C feature wrapper)."""
+    Z = np.empty((n, D), order="F")
+    b = np.empty((n, D), order="F")
+    check(lib().gpt_feature_inputs(n, D, int(seed) & (2 ** 64 - 1), _ptr(Z), _ptr(b)))
+    return Z, b
+
+
+def _feature_D(X, length_scale, sigma_RBF, phi_scale, Z, b):
+    X = _f64(X)
+    N, D = X.shape
+    Z = _f64(Z)
+    n = Z.shape[0]
+    if Z.shape != (n, D):
+        raise ValueError("Z must be (n, D)")
+    b = _f64(np.asarray(b, dtype=np.float64).reshape((n, D), order="F"))
+    ls = _f64(np.atleast_1d(length_scale))
+    if ls.size not in (1, D):
+        raise ValueError("dimensions of X and length_scale do not match")
+    phi = np.empty((n, D, N), order="F")
+    check(lib().gpt_feature(_ptr(X), N, D, _ptr(ls), ls.size, float(sigma_RBF), float(phi_scale),
+                            _ptr(Z), _ptr(b), n, _ptr(phi)))
+    return phi
+
+
+def feature(X, *args):
+    """Random Fourier features of the tensor model (all reference generations, see module doc)."""
+    if len(args) == 5 and np.ndim(args[3]) == 2:          # Gen D: ls, σ, phi_scale, Z, b
+        return _feature_D(X, *args)
+    if len(args) == 5:                                    # Gen C: n, ls, σ, seed, scale
+        n, ls, sigma, seed, scale = args
+        Z, b = feature_inputs(int(n), np.shape(X)[1], seed)
+        return _feature_D(X, ls, sigma, scale, Z, b)
+    if len(args) == 4:                                    # Gen B: n, ls, seed, scale
+        n, ls, seed, scale = args
+        Z, b = feature_inputs(int(n), np.shape(X)[1], seed)
+        return _feature_D(X, ls, 1.0, scale, Z, b)
+    if len(args) == 3:                                    # Gen A: n, ls, seed
+        n, ls, seed = args
+        Z, b = feature_inputs(int(n), np.shape(X)[1], seed)
+        return _feature_D(X, ls, 1.0, 1.0, Z, b)
+    raise TypeError("feature: unsupported argument list")
+
+
+def featureNotensor(X, *args):
+    """Full-theta RFF features (GPT_SGLD.jl:109-120); Gen C form draws Z, b from ``seed``."""
+    X = _f64(X)
+    N, D = X.shape
+    if len(args) != 4:
+        raise TypeError("featureNotensor: unsupported argument list")
+    if np.ndim(args[2]) != 2:                             # Gen C: n, ls, σ, seed
+        return featureNotensor_seeded(X, *args)
+    ls, sigma, Z, b = args                                # Gen D: ls, σ, Z, b
+    Z = _f64(Z)
+    b = _f64(np.asarray(b, dtype=np.float64).ravel())
+    n = Z.shape[0]
+    if Z.shape != (n, D) or b.size != n:
+        raise ValueError("Z must be (n, D) and b of length n")
+    ls = _f64(np.atleast_1d(ls))
+    phi = np.empty((n, N), order="F")
+    check(lib().gpt_feature_notensor(_ptr(X), N, D, _ptr(ls), ls.size, float(sigma), _ptr(Z),
+                                     _ptr(b), n, _ptr(phi)))
+    return phi
+
+
+def featureNotensor_seeded(X, n, length_scale, sigma_RBF, seed):
+    """Generation-C ``featureNotensor(X,n,ls,σ,seed)``: Z=randn(n,D), b=2π·rand(n)."""
+    X = _f64(X)
+    Z, b = feature_inputs(int(n), X.shape[1], seed)
+    return featureNotensor(X, length_scale, sigma_RBF, Z, b[:, 0])
+
+
+# ------------------------------------------------------------------ sparse core locations
+def samplenz(r, D, Q, seed=0):
+    """Q distinct lattice points of [r]^D (GPT_SGLD.jl:181-190), 1-based Int32 (Q, D)."""
+    I = np.empty((Q, D), dtype=np.int32, order="F")
+    check(lib().gpt_samplenz(r, D, Q, int(seed) & (2 ** 64 - 1), _ptr(I, P_I32)))
+    return I
+
+
+# ------------------------------------------------------------------ sampler
+def make_config(n, D, N, r, Q, m, epsw, epsU, signal_var, sigma_w, burnin, maxepoch, seed,
+                langevin=True, stiefel=True, store_every=1, max_steps=0):
+    return SGLDConfig(n=n, D=D, N=N, r=r, Q=Q, m=m, epsw=float(epsw), epsU=float(epsU),
+                      signal_var=float(signal_var), sigma_w=float(sigma_w), burnin=burnin,
+                      maxepoch=maxepoch, seed=int(seed) & (2 ** 64 - 1), langevin=int(bool(langevin)),
+                      stiefel=int(bool(stiefel)), store_every=store_every, max_steps=max_steps)
+
+
+def init_state(n, r, D, Q, seed, stiefel=True, sigma_w=1.0):
+    """Initial (w, U) GPTregression draws for ``param_seed`` (GPT_SGLD.jl:357-369)."""
+    cfg = make_config(n, D, 1, r, Q, 1, 0, 0, 1.0, sigma_w, 0, 1, seed, stiefel=stiefel)
+    w = np.empty(Q)
+    U = np.empty((n, r, D), order="F")
+    check(lib().gpt_sgld_init(C.byref(cfg), _ptr(w), _ptr(U)))
+    return w, U
+
+
+def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0,
+                  langevin=True, stiefel=True, sigma_w=1.0, store_every=1, max_steps=0,
+                  w_init=None, U_init=None, diag=False):
+    """Tensor-GP regression sampler (GPT_SGLD.jl:345-448).  Returns (w_store, U_store)
+    [, diag]; ``diag`` = per-step [‖gradw‖, ‖gradU_1‖, …] ((1+D) × steps)."""
+    phi = _f64(phi)
+    n, D, N = phi.shape
+    y = _f64(np.asarray(y, dtype=np.float64).ravel())
+    if y.size != N:
+        raise ValueError("phi and y disagree on N")
+    I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+    if I.shape != (Q, D):
+        raise ValueError("I must be (Q, D)")
+    cfg = make_config(n, D, N, r, Q, m, epsw, epsU, signal_var, sigma_w, burnin, maxepoch,
+                      param_seed, langevin, stiefel, store_every, max_steps)
+    nb = -(-N // m)
+    T = (maxepoch * nb) // store_every
+    w_store = np.zeros((Q, T), order="F")
+    U_store = np.zeros((n, r, D, T), order="F")
+    total = (burnin + maxepoch) * nb if max_steps <= 0 else min((burnin + maxepoch) * nb, max_steps)
+    dg = np.zeros((1 + D, total), order="F") if diag else None
+    wi = _f64(w_init) if w_init is not None else None
+    Ui = _f64(U_init) if U_init is not None else None
+    code = lib().gpt_sgld_regression(C.byref(cfg), _ptr(phi), _ptr(y), _ptr(I, P_I32),
+                                     _ptr(wi) if wi is not None else None,
+                                     _ptr(Ui) if Ui is not None else None,
+                                     _ptr(w_store), _ptr(U_store), _ptr(dg) if diag else None)
+    if code == _lib.GPT_ERR_NAN_GEODESIC:
+        print("Get NaN when moving along Geodesic. Try smaller epsU")
+        w_store[:] = 0.0
+        U_store[:] = 0.0
+    else:
+        check(code)
+    return (w_store, U_store, dg) if diag else (w_store, U_store)
+
+
+def GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0, **kw):
+    """Generation A/B sampler (GPT_SGLD_p.jl:146-243): ``sigma`` is the noise s.d. and the
+    prior s.d. of w is sqrt(n^D/Q) (:155)."""
+    n, D, _ = np.shape(phi)
+    return GPTregression(phi, y, float(sigma) ** 2, I, r, Q, m, epsw, epsU, burnin, maxepoch,
+                         param_seed, sigma_w=math.sqrt(float(n) ** D / Q), **kw)
+
+
+# ------------------------------------------------------------------ prediction
+def pred(w, U, I, phitest):
+    """fhat = pred(w, U, I, phitest) (GPT_SGLD.jl:233-243)."""
+    phitest = _f64(phitest)
+    n, D, Nt = phitest.shape
+    U = _f64(U)
+    r = U.shape[1]
+    w = _f64(np.asarray(w, dtype=np.float64).ravel())
+    I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+    out = np.empty(Nt)
+    check(lib().gpt_pred(_ptr(w), _ptr(U), _ptr(I, P_I32), _ptr(phitest), n, D, Nt, r, w.size,
+                         _ptr(out)))
+    return out
+
+
+def pred_mean(w_store, U_store, I, phitest, ytest, scale=1.0):
+    """Posterior-mean prediction over the stored samples and its RMSE·scale
+    (GPT_SGLD_p.jl:124-132; kin40kExperiment.jl:80-87).  Returns (meanfhat, rmse)."""
+    phitest = _f64(phitest)
+    n, D, Nt = phitest.shape
+    w_store = _f64(w_store)
+    U_store = _f64(U_store)
+    Q, S = w_store.shape
+    r = U_store.shape[1]
+    I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+    yt = _f64(np.asarray(ytest, dtype=np.float64).ravel())
+    mean = np.empty(Nt)
+    rm = C.c_double(0.0)
+    check(lib().gpt_pred_mean(_ptr(w_store), _ptr(U_store), _ptr(I, P_I32), _ptr(phitest), _ptr(yt),
+                              n, D, Nt, r, Q, S, float(scale), _ptr(mean), C.byref(rm)))
+    return mean, rm.value
+
+
+def RMSE(w_store, U_store, I, phitest, ytest):
+    """GPT_SGLD_p.jl:124-132: RMSE of the mean prediction over ALL stored samples."""
+    return pred_mean(w_store, U_store, I, phitest, ytest)[1]
+
+
+# ------------------------------------------------------------------ full-theta model
+def GPNT_SGLD(phi, y, signal_var, sigma_theta, m, eps_theta, decay_rate, burnin, maxepoch,
+              param_seed=0):
+    """Full-theta RFF SGLD (GPT_SGLD.jl:809-847).  Returns theta_store (n, T); on NaN prints
+    the reference's message and returns zeros(n) (:840-843)."""
+    phi = _f64(phi)
+    n, N = phi.shape
+    y = _f64(np.asarray(y, dtype=np.float64).ravel())
+    nb = -(-N // m)
+    out = np.empty((n, (maxepoch + burnin) * nb), order="F")
+    code = lib().gpt_gpnt_sgld(_ptr(phi), _ptr(y), n, N, float(signal_var), float(sigma_theta), m,
+                               float(eps_theta), float(decay_rate), burnin, maxepoch,
+                               int(param_seed) & (2 ** 64 - 1), _ptr(out))
+    if code == _lib.GPT_ERR_NAN_THETA:
+        print("Get NaN in theta. Try smaller epsilon")
+        return np.zeros(n)
+    check(code)
+    return out

@@ -1,0 +1,711 @@
+// Host side of libgptsgld.so: the C ABI of include/gptsgld.h.
+//
+// Replaces the Julia module API of GPT_SGLD.jl (feature :71, featureNotensor :109, samplenz :181,
+// GPTregression :345, pred :233, GPNT_SGLD :809) and GPT_SGLD_p.jl (GPT_SGLDERM :146, RMSE :124).
+// All arithmetic of the sampler runs in the HIP kernels; the host only validates arguments,
+// draws the one-time initial state and the epoch permutations from the Philox contract (the
+// reference does the same draws on the CPU, GPT_SGLD.jl:357-373), moves buffers and launches.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gpt_internal.h"
+
+namespace gpt {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+int hip_fail(hipError_t e, const char* what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return GPT_ERR_HIP;
+}
+hipError_t set_lds_limits();
+size_t pred_lds_bytes(int n, int D, int r, int Q);
+
+#define HIPCHK(call)                                   \
+  do {                                                 \
+    hipError_t _e = (call);                            \
+    if (_e != hipSuccess) return hip_fail(_e, #call);  \
+  } while (0)
+
+// ------------------------------------------------------------------ host Philox consumers
+static double host_normal(uint64_t seed, uint32_t e, uint32_t c1, uint32_t c2, uint32_t c3) {
+  const U4 x = philox4x32(e >> 1, c1, c2, c3, seed);
+  const double u1 = u53(x.x, x.y), u2 = u53(x.z, x.w);
+  const double rad = std::sqrt(-2.0 * std::log(u1));
+  const double th = 6.283185307179586 * u2;
+  return (e & 1u) ? rad * std::sin(th) : rad * std::cos(th);
+}
+
+// Cyclic Jacobi eigendecomposition of a symmetric r×r matrix (row-major, destroyed).
+static void jacobi_eig(int r, std::vector<double>& A, std::vector<double>& V,
+                       std::vector<double>& ev) {
+  V.assign((size_t)r * r, 0.0);
+  for (int i = 0; i < r; ++i) V[i * r + i] = 1.0;
+  for (int sweep = 0; sweep < 100; ++sweep) {
+    double off = 0.0, tot = 0.0;
+    for (int i = 0; i < r; ++i)
+      for (int j = 0; j < r; ++j) {
+        tot += A[i * r + j] * A[i * r + j];
+        if (i != j) off += A[i * r + j] * A[i * r + j];
+      }
+    if (off <= 1e-32 * tot) break;
+    for (int p = 0; p < r; ++p)
+      for (int q = p + 1; q < r; ++q) {
+        const double apq = A[p * r + q];
+        if (apq == 0.0) continue;
+        const double theta = (A[q * r + q] - A[p * r + p]) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+        const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < r; ++k) {  // A = Jᵀ A J
+          const double akp = A[k * r + p], akq = A[k * r + q];
+          A[k * r + p] = c * akp - s * akq;
+          A[k * r + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < r; ++k) {
+          const double apk = A[p * r + k], aqk = A[q * r + k];
+          A[p * r + k] = c * apk - s * aqk;
+          A[q * r + k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < r; ++k) {
+          const double vkp = V[k * r + p], vkq = V[k * r + q];
+          V[k * r + p] = c * vkp - s * vkq;
+          V[k * r + q] = s * vkp + c * vkq;
+        }
+      }
+  }
+  ev.resize(r);
+  for (int i = 0; i < r; ++i) ev[i] = A[i * r + i];
+}
+
+// GPT_SGLD.jl:357-369: w = σ_w·randn(Q); U_k = Zᵀ(ZZᵀ)^(-1/2), Z = randn(r,n)  (or randn/√n).
+void host_init_state(int n, int r, int D, int Q, uint64_t seed, bool stiefel, double sigma_w,
+                     double* w, double* U) {
+  for (int q = 0; q < Q; ++q) w[q] = sigma_w * host_normal(seed, q, 0, kWInit, 0);
+  std::vector<double> Z((size_t)r * n), G, Vv, ev;
+  for (int k = 0; k < D; ++k) {
+    for (int e = 0; e < r * n; ++e) Z[e] = host_normal(seed, e, 0, kUInit, k);  // Z[a + r*j]
+    double* Uk = U + (size_t)n * r * k;
+    if (!stiefel) {
+      for (int j = 0; j < n; ++j)
+        for (int a = 0; a < r; ++a) Uk[j + (size_t)n * a] = Z[a + (size_t)r * j] / std::sqrt((double)n);
+      continue;
+    }
+    G.assign((size_t)r * r, 0.0);
+    for (int a = 0; a < r; ++a)
+      for (int c = 0; c < r; ++c) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) s += Z[a + (size_t)r * j] * Z[c + (size_t)r * j];
+        G[a * r + c] = s;
+      }
+    jacobi_eig(r, G, Vv, ev);
+    std::vector<double> S((size_t)r * r, 0.0);  // (ZZᵀ)^(-1/2)
+    for (int a = 0; a < r; ++a)
+      for (int c = 0; c < r; ++c) {
+        double s = 0.0;
+        for (int z = 0; z < r; ++z) s += Vv[a * r + z] * Vv[c * r + z] / std::sqrt(ev[z]);
+        S[a * r + c] = s;
+      }
+    for (int j = 0; j < n; ++j)
+      for (int c = 0; c < r; ++c) {
+        double s = 0.0;
+        for (int a = 0; a < r; ++a) s += Z[a + (size_t)r * j] * S[a * r + c];
+        Uk[j + (size_t)n * c] = s;
+      }
+  }
+}
+
+// Cumulative epoch orders: phi=phi[:,:,perm] every epoch composes the permutations
+// (GPT_SGLD.jl:373-374); order_e = order_{e-1}[perm_e], perm_e Fisher–Yates on PERM stream.
+void host_epoch_orders(int N, uint64_t seed, int epochs, int32_t* out) {
+  std::vector<int32_t> cur(N), p(N);
+  for (int i = 0; i < N; ++i) cur[i] = i;
+  for (int e = 0; e < epochs; ++e) {
+    for (int i = 0; i < N; ++i) p[i] = i;
+    for (int i = N - 1; i >= 1; --i) {
+      const uint32_t x = philox4x32((uint32_t)i, (uint32_t)e, kPerm, 0, seed).x;
+      const int j = (int)(((uint64_t)x * (uint64_t)(i + 1)) >> 32);
+      std::swap(p[i], p[j]);
+    }
+    int32_t* o = out + (size_t)e * N;
+    for (int i = 0; i < N; ++i) o[i] = cur[p[i]];
+    std::memcpy(cur.data(), o, sizeof(int32_t) * N);
+  }
+}
+
+struct DevMem {
+  void* p = nullptr;
+  DevMem() = default;
+  DevMem(const DevMem&) = delete;
+  DevMem& operator=(const DevMem&) = delete;
+  ~DevMem() { if (p) (void)hipFree(p); }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 16); }
+  template <class T> T* as() const { return (T*)p; }
+};
+
+static bool valid_cfg(const gpt_sgld_config* c) {
+  if (!c) { set_error("null config"); return false; }
+  if (c->n < 1 || c->D < 1 || c->N < 1 || c->r < 1 || c->Q < 1 || c->m < 1) {
+    set_error("dimensions must be positive"); return false;
+  }
+  if (c->D > kDMax) { set_error("D > 16 is not supported by the kernels"); return false; }
+  if (!rank_supported((int)c->r)) {
+    set_error("rank r not instantiated (supported: 1-6,8,10,12,15,16,20)"); return false;
+  }
+  if (c->n > (1 << 20) || c->N > (1LL << 31) - 1 || c->Q > (1 << 20)) {
+    set_error("dimension too large"); return false;
+  }
+  double rD = std::pow((double)c->r, (double)c->D);
+  if ((double)c->Q > rD) { set_error("Q must be <= r^D"); return false; }
+  if (c->store_every < 1) { set_error("store_every must be >= 1"); return false; }
+  if (!(c->signal_var > 0) || !(c->sigma_w > 0)) { set_error("variances must be > 0"); return false; }
+  const StepLayout L = step_layout((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m);
+  if (L.bytes > 160 * 1024) {
+    set_error("working set exceeds 160 KiB LDS (n*r, Q*D or m too large)"); return false;
+  }
+  return true;
+}
+
+}  // namespace gpt
+
+using namespace gpt;
+
+// ====================================================================== session
+struct gpt_sgld_session {
+  gpt_sgld_config cfg{};
+  int nchains = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  StepParams P{};
+  long long numbatches = 0, total_steps = 0, steps_done = 0, nstore = 0;
+  int epochs = 0;
+  DevMem I0, chains_d, tbase, status;
+  std::vector<std::unique_ptr<DevMem>> chain_mem;
+  std::vector<ChainDesc> chains_h;
+  bool temp_ready = false;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  int graph_steps = 0;
+  bool store = false, diag = false;
+};
+
+extern "C" const char* gpt_last_error(void) { return g_err.c_str(); }
+
+extern "C" int gpt_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+static int session_enqueue(gpt_sgld_session* s, int count) {
+  for (int i = 0; i < count; ++i) {
+    hipError_t e = launch_step(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
+                               s->tbase.as<long long>(), i, s->stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_step");
+  }
+  hipError_t e = launch_advance(s->tbase.as<long long>(), count, s->stream);
+  if (e != hipSuccess) return hip_fail(e, "launch_advance");
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchains,
+                                       const uint64_t* seeds, const double* const* phi_dev,
+                                       const double* const* y_dev, const int32_t* I_host,
+                                       int32_t store_flags, void* hip_stream,
+                                       gpt_sgld_session** out) {
+  if (!out) { set_error("null out"); return GPT_ERR_BAD_DIMS; }
+  *out = nullptr;
+  if (!valid_cfg(cfg)) return GPT_ERR_BAD_DIMS;
+  if (nchains < 1 || !seeds || !phi_dev || !y_dev || !I_host) {
+    set_error("bad chain arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  const int n = (int)cfg->n, D = (int)cfg->D, N = (int)cfg->N, r = (int)cfg->r, Q = (int)cfg->Q,
+            m = (int)cfg->m;
+  for (long long x = 0; x < (long long)Q * D; ++x)
+    if (I_host[x] < 1 || I_host[x] > r) { set_error("I entries must be in 1..r"); return GPT_ERR_BAD_DIMS; }
+  hipError_t he = set_lds_limits();
+  if (he != hipSuccess) return hip_fail(he, "hipFuncSetAttribute");
+
+  std::unique_ptr<gpt_sgld_session> s(new gpt_sgld_session());
+  s->cfg = *cfg;
+  s->nchains = nchains;
+  s->numbatches = (N + m - 1) / m;
+  s->epochs = (int)(cfg->burnin + cfg->maxepoch);
+  s->total_steps = (long long)s->epochs * s->numbatches;
+  if (cfg->max_steps > 0) s->total_steps = std::min<long long>(s->total_steps, cfg->max_steps);
+  s->nstore = (cfg->maxepoch * s->numbatches) / cfg->store_every;
+  s->store = (store_flags & 1) != 0;
+  s->diag = (store_flags & 2) != 0;
+  if (hip_stream) s->stream = (hipStream_t)hip_stream;
+  else {
+    HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    s->own_stream = true;
+  }
+  StepParams& P = s->P;
+  P.n = n; P.D = D; P.N = N; P.r = r; P.Q = Q; P.m = m; P.nb = (int)s->numbatches;
+  P.burnin_steps = (int)(cfg->burnin * s->numbatches);
+  P.total_steps = s->total_steps;
+  P.store_every = (int)cfg->store_every;
+  P.langevin = cfg->langevin; P.stiefel = cfg->stiefel;
+  P.signal_var = cfg->signal_var; P.sigma_w = cfg->sigma_w; P.epsw = cfg->epsw; P.epsU = cfg->epsU;
+
+  std::vector<int32_t> I0((size_t)Q * D);
+  for (size_t x = 0; x < I0.size(); ++x) I0[x] = I_host[x] - 1;
+  HIPCHK(s->I0.alloc(sizeof(int32_t) * I0.size()));
+  HIPCHK(hipMemcpy(s->I0.p, I0.data(), sizeof(int32_t) * I0.size(), hipMemcpyHostToDevice));
+  P.I0 = s->I0.as<int32_t>();
+  HIPCHK(s->tbase.alloc(sizeof(long long)));
+  HIPCHK(hipMemset(s->tbase.p, 0, sizeof(long long)));
+  HIPCHK(s->status.alloc(sizeof(int32_t) * nchains));
+  HIPCHK(hipMemset(s->status.p, 0, sizeof(int32_t) * nchains));
+
+  constexpr size_t a = 256;
+  auto up = [](size_t x) { return (x + a - 1) / a * a; };
+  const size_t b_w = up(8 * 2 * (size_t)Q), b_U = up(8 * (size_t)n * r * D),
+               b_temp = up(8 * 2 * (size_t)D * r * m),
+               b_ord = up(4 * (size_t)s->epochs * N),
+               b_ws = s->store ? up(8 * (size_t)Q * s->nstore) : 0,
+               b_Us = s->store ? up(8 * (size_t)n * r * D * s->nstore) : 0,
+               b_dg = s->diag ? up(8 * (size_t)(1 + D) * s->total_steps) : 0;
+  std::vector<double> w0(Q), U0((size_t)n * r * D);
+  std::vector<int32_t> ord((size_t)s->epochs * N);
+  s->chains_h.resize(nchains);
+  for (int c = 0; c < nchains; ++c) {
+    std::unique_ptr<DevMem> mem(new DevMem());
+    HIPCHK(mem->alloc(b_w + b_U + b_temp + b_ord + b_ws + b_Us + b_dg));
+    char* base = mem->as<char>();
+    ChainDesc& C = s->chains_h[c];
+    C.phi = phi_dev[c];
+    C.y = y_dev[c];
+    C.w = (double*)base;
+    C.U = (double*)(base + b_w);
+    C.temp = (double*)(base + b_w + b_U);
+    C.order = (const int32_t*)(base + b_w + b_U + b_temp);
+    C.w_store = s->store ? (double*)(base + b_w + b_U + b_temp + b_ord) : nullptr;
+    C.U_store = s->store ? (double*)(base + b_w + b_U + b_temp + b_ord + b_ws) : nullptr;
+    C.diag = s->diag ? (double*)(base + b_w + b_U + b_temp + b_ord + b_ws + b_Us) : nullptr;
+    C.status = s->status.as<int32_t>() + c;
+    C.seed = seeds[c];
+    host_init_state(n, r, D, Q, seeds[c], cfg->stiefel != 0, cfg->sigma_w, w0.data(), U0.data());
+    host_epoch_orders(N, seeds[c], s->epochs, ord.data());
+    HIPCHK(hipMemcpy(C.w, w0.data(), 8 * (size_t)Q, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(C.U, U0.data(), 8 * U0.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void*)C.order, ord.data(), 4 * ord.size(), hipMemcpyHostToDevice));
+    if (s->store) HIPCHK(hipMemset(C.w_store, 0, b_ws + b_Us));
+    if (s->diag) HIPCHK(hipMemset(C.diag, 0, b_dg));
+    s->chain_mem.push_back(std::move(mem));
+  }
+  HIPCHK(s->chains_d.alloc(sizeof(ChainDesc) * nchains));
+  HIPCHK(hipMemcpy(s->chains_d.p, s->chains_h.data(), sizeof(ChainDesc) * nchains,
+                   hipMemcpyHostToDevice));
+  s->graph_steps = (int)std::min<long long>(std::max<long long>(s->numbatches, 1), 512);
+  *out = s.release();
+  return GPT_OK;
+}
+
+// Overwrite chain c's initial state (w_init/U_init injection of the host API).
+static int session_set_state(gpt_sgld_session* s, int c, const double* w, const double* U) {
+  const ChainDesc& C = s->chains_h[c];
+  if (w) HIPCHK(hipMemcpy(C.w, w, 8 * (size_t)s->P.Q, hipMemcpyHostToDevice));
+  if (U) HIPCHK(hipMemcpy(C.U, U, 8 * (size_t)s->P.n * s->P.r * s->P.D, hipMemcpyHostToDevice));
+  s->temp_ready = false;
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps) {
+  if (!s) { set_error("null session"); return GPT_ERR_BAD_DIMS; }
+  long long remaining = std::min<long long>(nsteps, s->total_steps - s->steps_done);
+  if (remaining <= 0) return GPT_OK;
+  if (!s->temp_ready) {
+    hipError_t e = launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
+                                    s->tbase.as<long long>(), s->stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_temp_init");
+    s->temp_ready = true;
+  }
+  while (remaining > 0) {
+    const int chunk = (int)std::min<long long>(remaining, s->graph_steps);
+    if (chunk == s->graph_steps) {
+      if (!s->gexec) {
+        HIPCHK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+        int rc = session_enqueue(s, chunk);
+        hipGraph_t g = nullptr;
+        hipError_t ee = hipStreamEndCapture(s->stream, &g);
+        if (rc != GPT_OK) return rc;
+        if (ee != hipSuccess) return hip_fail(ee, "hipStreamEndCapture");
+        s->graph = g;
+        HIPCHK(hipGraphInstantiate(&s->gexec, s->graph, nullptr, nullptr, 0));
+      }
+      HIPCHK(hipGraphLaunch(s->gexec, s->stream));
+    } else {
+      int rc = session_enqueue(s, chunk);
+      if (rc != GPT_OK) return rc;
+    }
+    s->steps_done += chunk;
+    remaining -= chunk;
+  }
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, double* avg_us) {
+  if (!s) { set_error("null session"); return GPT_ERR_BAD_DIMS; }
+  const long long cnt = std::min<long long>(nsteps, s->total_steps - s->steps_done);
+  if (avg_us) *avg_us = 0.0;
+  if (cnt <= 0) return GPT_OK;
+  if (!s->temp_ready) {
+    hipError_t e = launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
+                                    s->tbase.as<long long>(), s->stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_temp_init");
+    s->temp_ready = true;
+  }
+  std::vector<hipEvent_t> ev(2 * cnt, nullptr);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  int rc = GPT_OK;
+  for (long long i = 0; i < cnt && rc == GPT_OK; ++i) {
+    HIPCHK(hipEventRecord(ev[2 * i], s->stream));
+    hipError_t e = launch_step(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
+                               s->tbase.as<long long>(), (int)i, s->stream);
+    if (e != hipSuccess) rc = hip_fail(e, "launch_step");
+    HIPCHK(hipEventRecord(ev[2 * i + 1], s->stream));
+  }
+  if (rc == GPT_OK) {
+    hipError_t e = launch_advance(s->tbase.as<long long>(), cnt, s->stream);
+    if (e != hipSuccess) rc = hip_fail(e, "launch_advance");
+  }
+  HIPCHK(hipStreamSynchronize(s->stream));
+  double tot = 0.0;
+  for (long long i = 0; i < cnt; ++i) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+    tot += ms;
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  if (rc != GPT_OK) return rc;
+  s->steps_done += cnt;
+  if (avg_us) *avg_us = 1000.0 * tot / (double)cnt;
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_sync(gpt_sgld_session* s) {
+  if (!s) return GPT_ERR_BAD_DIMS;
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return GPT_OK;
+}
+
+extern "C" int64_t gpt_sgld_session_steps_done(gpt_sgld_session* s) { return s ? s->steps_done : -1; }
+
+extern "C" int gpt_sgld_session_state(gpt_sgld_session* s, int32_t chain, double** w_dev,
+                                      double** U_dev, double** w_store_dev, double** U_store_dev,
+                                      int64_t* nstore) {
+  if (!s || chain < 0 || chain >= s->nchains) { set_error("bad chain"); return GPT_ERR_BAD_DIMS; }
+  const ChainDesc& C = s->chains_h[chain];
+  // current w lives in the ping-pong slot of the next step
+  if (w_dev) *w_dev = C.w + (size_t)(s->steps_done & 1) * s->P.Q;
+  if (U_dev) *U_dev = C.U;
+  if (w_store_dev) *w_store_dev = C.w_store;
+  if (U_store_dev) *U_store_dev = C.U_store;
+  if (nstore) *nstore = s->nstore;
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double* w_store,
+                                      double* U_store, double* diag, int32_t* status) {
+  if (!s || chain < 0 || chain >= s->nchains) { set_error("bad chain"); return GPT_ERR_BAD_DIMS; }
+  HIPCHK(hipStreamSynchronize(s->stream));
+  const ChainDesc& C = s->chains_h[chain];
+  int32_t st = 0;
+  HIPCHK(hipMemcpy(&st, C.status, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (status) *status = st;
+  const size_t nws = (size_t)s->P.Q * s->nstore, nus = (size_t)s->P.n * s->P.r * s->P.D * s->nstore;
+  if (w_store) {
+    if (!s->store) { set_error("session created without stores"); return GPT_ERR_BAD_DIMS; }
+    if (st) std::memset(w_store, 0, 8 * nws);  // GPT_SGLD.jl:422-424
+    else HIPCHK(hipMemcpy(w_store, C.w_store, 8 * nws, hipMemcpyDeviceToHost));
+  }
+  if (U_store) {
+    if (!s->store) { set_error("session created without stores"); return GPT_ERR_BAD_DIMS; }
+    if (st) std::memset(U_store, 0, 8 * nus);
+    else HIPCHK(hipMemcpy(U_store, C.U_store, 8 * nus, hipMemcpyDeviceToHost));
+  }
+  if (diag) {
+    if (!s->diag) { set_error("session created without diagnostics"); return GPT_ERR_BAD_DIMS; }
+    HIPCHK(hipMemcpy(diag, C.diag, 8 * (size_t)(1 + s->P.D) * s->total_steps, hipMemcpyDeviceToHost));
+  }
+  return GPT_OK;
+}
+
+extern "C" void gpt_sgld_session_destroy(gpt_sgld_session* s) {
+  if (!s) return;
+  (void)hipStreamSynchronize(s->stream);
+  if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+  if (s->graph) (void)hipGraphDestroy(s->graph);
+  if (s->own_stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+// ====================================================================== host-pointer API
+extern "C" int gpt_sgld_init(const gpt_sgld_config* cfg, double* w_out, double* U_out) {
+  if (!valid_cfg(cfg)) return GPT_ERR_BAD_DIMS;
+  host_init_state((int)cfg->n, (int)cfg->r, (int)cfg->D, (int)cfg->Q, cfg->seed, cfg->stiefel != 0,
+                  cfg->sigma_w, w_out, U_out);
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi, const double* y,
+                                   const int32_t* I, const double* w_init, const double* U_init,
+                                   double* w_store, double* U_store, double* diag) {
+  if (!valid_cfg(cfg)) return GPT_ERR_BAD_DIMS;
+  if (!phi || !y || !I) { set_error("null input"); return GPT_ERR_BAD_DIMS; }
+  const size_t nphi = (size_t)cfg->n * cfg->D * cfg->N;
+  DevMem dphi, dy;
+  HIPCHK(dphi.alloc(8 * nphi));
+  HIPCHK(dy.alloc(8 * (size_t)cfg->N));
+  HIPCHK(hipMemcpy(dphi.p, phi, 8 * nphi, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy.p, y, 8 * (size_t)cfg->N, hipMemcpyHostToDevice));
+  const double* pp = dphi.as<double>();
+  const double* yy = dy.as<double>();
+  gpt_sgld_session* s = nullptr;
+  const int flags = ((w_store || U_store) ? 1 : 0) | (diag ? 2 : 0);
+  int rc = gpt_sgld_session_create(cfg, 1, &cfg->seed, &pp, &yy, I, flags, nullptr, &s);
+  if (rc != GPT_OK) return rc;
+  std::unique_ptr<gpt_sgld_session, void (*)(gpt_sgld_session*)> guard(s, gpt_sgld_session_destroy);
+  if (w_init || U_init) {
+    rc = session_set_state(s, 0, w_init, U_init);
+    if (rc != GPT_OK) return rc;
+  }
+  rc = gpt_sgld_session_run(s, s->total_steps);
+  if (rc != GPT_OK) return rc;
+  int32_t st = 0;
+  rc = gpt_sgld_session_fetch(s, 0, w_store, U_store, diag, &st);
+  if (rc != GPT_OK) return rc;
+  if (st) {
+    set_error("Get NaN when moving along Geodesic. Try smaller epsU");
+    return GPT_ERR_NAN_GEODESIC;
+  }
+  return GPT_OK;
+}
+
+extern "C" int gpt_samplenz(int64_t r, int64_t D, int64_t Q, uint64_t seed, int32_t* I_out) {
+  if (r < 1 || D < 1 || Q < 1 || !I_out) { set_error("bad samplenz arguments"); return GPT_ERR_BAD_DIMS; }
+  unsigned __int128 M = 1;
+  for (int k = 0; k < D; ++k) {
+    M *= (unsigned __int128)r;
+    if (M > ((unsigned __int128)1 << 62)) { set_error("r^D too large"); return GPT_ERR_BAD_DIMS; }
+  }
+  if ((unsigned __int128)Q > M) { set_error("Q must be <= r^D"); return GPT_ERR_BAD_DIMS; }
+  const uint64_t MM = (uint64_t)M;
+  std::unordered_map<uint64_t, uint64_t> sw;
+  auto get = [&sw](uint64_t x) { auto it = sw.find(x); return it == sw.end() ? x : it->second; };
+  for (int64_t i = 0; i < Q; ++i) {
+    const U4 x = philox4x32((uint32_t)i, 0, kSampleNZ, 0, seed);
+    const uint64_t u = ((uint64_t)x.x << 32) | x.y;
+    const uint64_t j = (uint64_t)i + (uint64_t)(((unsigned __int128)u * (MM - (uint64_t)i)) >> 64);
+    const uint64_t vi = get(i), vj = get(j);
+    sw[i] = vj;
+    sw[j] = vi;
+    uint64_t v = vj;  // L[i]; I[i,:] = digits(L, r, D) + 1
+    for (int64_t k = 0; k < D; ++k) {
+      I_out[i + Q * k] = (int32_t)(v % (uint64_t)r) + 1;
+      v /= (uint64_t)r;
+    }
+  }
+  return GPT_OK;
+}
+
+extern "C" int gpt_feature_inputs(int64_t n, int64_t D, uint64_t seed, double* Z_out, double* b_out) {
+  if (n < 1 || D < 1) { set_error("bad dims"); return GPT_ERR_BAD_DIMS; }
+  for (int64_t e = 0; e < n * D; ++e) {
+    if (Z_out) Z_out[e] = host_normal(seed, (uint32_t)e, 0, kFeatZ, 0);
+    if (b_out) {
+      const U4 x = philox4x32((uint32_t)e, 0, kFeatB, 0, seed);
+      b_out[e] = 2.0 * 3.141592653589793 * u53(x.x, x.y);
+    }
+  }
+  return GPT_OK;
+}
+
+static int feature_common(bool tensor, const double* X, int64_t N, int64_t D, const double* ls,
+                          int64_t ls_len, double sigma_rbf, double phi_scale, const double* Z,
+                          const double* b, int64_t n, double* phi_out) {
+  if (!X || !ls || !Z || !b || !phi_out || N < 1 || D < 1 || n < 1) {
+    set_error("bad feature arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  if (ls_len != 1 && ls_len != D) {
+    set_error("dimensions of X and length_scale do not match"); return GPT_ERR_BAD_DIMS;
+  }
+  std::vector<double> lsv(D);
+  for (int64_t k = 0; k < D; ++k) lsv[k] = ls[ls_len == 1 ? 0 : k];
+  const size_t nphi = tensor ? (size_t)n * D * N : (size_t)n * N;
+  const size_t nb = tensor ? (size_t)n * D : (size_t)n;
+  DevMem dX, dls, dZ, db, dphi;
+  HIPCHK(dX.alloc(8 * (size_t)N * D));
+  HIPCHK(dls.alloc(8 * (size_t)D));
+  HIPCHK(dZ.alloc(8 * (size_t)n * D));
+  HIPCHK(db.alloc(8 * nb));
+  HIPCHK(dphi.alloc(8 * nphi));
+  HIPCHK(hipMemcpy(dX.p, X, 8 * (size_t)N * D, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dls.p, lsv.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dZ.p, Z, 8 * (size_t)n * D, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(db.p, b, 8 * nb, hipMemcpyHostToDevice));
+  hipError_t e;
+  if (tensor) {
+    const double c = phi_scale * std::pow(sigma_rbf, 1.0 / (double)D) * std::sqrt(2.0 / (double)n);
+    e = launch_feature(dX.as<double>(), N, (int)D, dls.as<double>(), c, dZ.as<double>(),
+                       db.as<double>(), (int)n, dphi.as<double>(), nullptr);
+  } else {
+    const double c = std::sqrt(2.0 / (double)n) * sigma_rbf;
+    e = launch_feature_notensor(dX.as<double>(), N, (int)D, dls.as<double>(), c, dZ.as<double>(),
+                                db.as<double>(), (int)n, dphi.as<double>(), nullptr);
+  }
+  if (e != hipSuccess) return hip_fail(e, "feature kernel");
+  HIPCHK(hipMemcpy(phi_out, dphi.p, 8 * nphi, hipMemcpyDeviceToHost));
+  return GPT_OK;
+}
+
+extern "C" int gpt_feature_dev(const double* X_dev, int64_t N, int64_t D, const double* ls_dev,
+                               int64_t ls_len, double sigma_rbf, double phi_scale,
+                               const double* Z_dev, const double* b_dev, int64_t n, double* phi_dev,
+                               void* hip_stream) {
+  if (!X_dev || !ls_dev || !Z_dev || !b_dev || !phi_dev || N < 1 || D < 1 || n < 1 || ls_len != D) {
+    set_error("bad gpt_feature_dev arguments (ls_len must equal D)"); return GPT_ERR_BAD_DIMS;
+  }
+  const double c = phi_scale * std::pow(sigma_rbf, 1.0 / (double)D) * std::sqrt(2.0 / (double)n);
+  hipError_t e = launch_feature(X_dev, N, (int)D, ls_dev, c, Z_dev, b_dev, (int)n, phi_dev,
+                                (hipStream_t)hip_stream);
+  if (e != hipSuccess) return hip_fail(e, "feature kernel");
+  return GPT_OK;
+}
+
+extern "C" int gpt_feature(const double* X, int64_t N, int64_t D, const double* length_scale,
+                           int64_t ls_len, double sigma_rbf, double phi_scale, const double* Z,
+                           const double* b, int64_t n, double* phi_out) {
+  return feature_common(true, X, N, D, length_scale, ls_len, sigma_rbf, phi_scale, Z, b, n, phi_out);
+}
+
+extern "C" int gpt_feature_notensor(const double* X, int64_t N, int64_t D, const double* length_scale,
+                                    int64_t ls_len, double sigma_rbf, const double* Z,
+                                    const double* b, int64_t n, double* phi_out) {
+  return feature_common(false, X, N, D, length_scale, ls_len, sigma_rbf, 1.0, Z, b, n, phi_out);
+}
+
+static bool valid_pred(int64_t n, int64_t D, int64_t Ntest, int64_t r, int64_t Q) {
+  if (n < 1 || D < 1 || Ntest < 0 || r < 1 || Q < 1) { set_error("bad pred dims"); return false; }
+  if (D > kDMax) { set_error("D > 16 unsupported"); return false; }
+  if (!rank_supported((int)r)) { set_error("rank not instantiated"); return false; }
+  if (pred_lds_bytes((int)n, (int)D, (int)r, (int)Q) > 160 * 1024) { set_error("pred LDS too large"); return false; }
+  return true;
+}
+
+extern "C" int gpt_pred_dev(const double* w_dev, const double* U_dev, const int32_t* I0_dev,
+                            const double* phitest_dev, int64_t n, int64_t D, int64_t Ntest,
+                            int64_t r, int64_t Q, int64_t S, double* fhat_dev, void* hip_stream) {
+  if (!valid_pred(n, D, Ntest, r, Q)) return GPT_ERR_BAD_DIMS;
+  hipError_t e = launch_pred(w_dev, U_dev, I0_dev, phitest_dev, (int)n, (int)D, Ntest, (int)r,
+                             (int)Q, (int)S, fhat_dev, (hipStream_t)hip_stream);
+  if (e != hipSuccess) return hip_fail(e, "pred kernel");
+  return GPT_OK;
+}
+
+static int pred_host(const double* w, const double* U, const int32_t* I, const double* phitest,
+                     const double* ytest, int64_t n, int64_t D, int64_t Ntest, int64_t r,
+                     int64_t Q, int64_t S, double scale, double* fhat_out, double* mean_out,
+                     double* rmse_out) {
+  if (!valid_pred(n, D, Ntest, r, Q) || S < 1) return GPT_ERR_BAD_DIMS;
+  std::vector<int32_t> I0((size_t)Q * D);
+  for (size_t x = 0; x < I0.size(); ++x) {
+    if (I[x] < 1 || I[x] > r) { set_error("I entries must be in 1..r"); return GPT_ERR_BAD_DIMS; }
+    I0[x] = I[x] - 1;
+  }
+  DevMem dw, dU, dI, dphi, df, dy, dmean, dsse;
+  HIPCHK(dw.alloc(8 * (size_t)Q * S));
+  HIPCHK(dU.alloc(8 * (size_t)n * r * D * S));
+  HIPCHK(dI.alloc(4 * I0.size()));
+  HIPCHK(dphi.alloc(8 * (size_t)n * D * Ntest));
+  HIPCHK(df.alloc(8 * (size_t)Ntest * S));
+  HIPCHK(hipMemcpy(dw.p, w, 8 * (size_t)Q * S, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dU.p, U, 8 * (size_t)n * r * D * S, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dI.p, I0.data(), 4 * I0.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dphi.p, phitest, 8 * (size_t)n * D * Ntest, hipMemcpyHostToDevice));
+  int rc = gpt_pred_dev(dw.as<double>(), dU.as<double>(), dI.as<int32_t>(), dphi.as<double>(), n,
+                        D, Ntest, r, Q, S, df.as<double>(), nullptr);
+  if (rc != GPT_OK) return rc;
+  if (fhat_out) HIPCHK(hipMemcpy(fhat_out, df.p, 8 * (size_t)Ntest * S, hipMemcpyDeviceToHost));
+  if (ytest) {
+    HIPCHK(dy.alloc(8 * (size_t)Ntest));
+    HIPCHK(dmean.alloc(8 * (size_t)Ntest));
+    HIPCHK(dsse.alloc(8 * (size_t)(S + 1)));
+    HIPCHK(hipMemcpy(dy.p, ytest, 8 * (size_t)Ntest, hipMemcpyHostToDevice));
+    hipError_t e = launch_mean_rmse(df.as<double>(), dy.as<double>(), Ntest, (int)S,
+                                    dmean.as<double>(), dsse.as<double>(), nullptr);
+    if (e != hipSuccess) return hip_fail(e, "mean/sse kernel");
+    double sse = 0.0;
+    HIPCHK(hipMemcpy(&sse, dsse.p, 8, hipMemcpyDeviceToHost));
+    if (mean_out) HIPCHK(hipMemcpy(mean_out, dmean.p, 8 * (size_t)Ntest, hipMemcpyDeviceToHost));
+    if (rmse_out) *rmse_out = scale * std::sqrt(sse / (double)Ntest);
+  }
+  HIPCHK(hipDeviceSynchronize());
+  return GPT_OK;
+}
+
+extern "C" int gpt_pred(const double* w, const double* U, const int32_t* I, const double* phitest,
+                        int64_t n, int64_t D, int64_t Ntest, int64_t r, int64_t Q, double* fhat_out) {
+  return pred_host(w, U, I, phitest, nullptr, n, D, Ntest, r, Q, 1, 1.0, fhat_out, nullptr, nullptr);
+}
+
+extern "C" int gpt_pred_mean(const double* w_store, const double* U_store, const int32_t* I,
+                             const double* phitest, const double* ytest, int64_t n, int64_t D,
+                             int64_t Ntest, int64_t r, int64_t Q, int64_t S, double scale,
+                             double* mean_out, double* rmse_out) {
+  if (!ytest) { set_error("ytest required"); return GPT_ERR_BAD_DIMS; }
+  return pred_host(w_store, U_store, I, phitest, ytest, n, D, Ntest, r, Q, S, scale, nullptr,
+                   mean_out, rmse_out);
+}
+
+extern "C" int gpt_gpnt_sgld(const double* phi, const double* y, int64_t n, int64_t N,
+                             double signal_var, double sigma_theta, int64_t m, double eps_theta,
+                             double decay_rate, int64_t burnin, int64_t maxepoch, uint64_t seed,
+                             double* theta_store) {
+  if (!phi || !y || !theta_store || n < 1 || N < 1 || m < 1 || burnin < 0 || maxepoch < 0) {
+    set_error("bad GPNT_SGLD arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  const long long nb = (N + m - 1) / m;
+  const int epochs = (int)(burnin + maxepoch);
+  const long long total = (long long)epochs * nb;
+  std::vector<double> th0(n);
+  for (int64_t j = 0; j < n; ++j) th0[j] = sigma_theta * host_normal(seed, (uint32_t)j, 0, kThetaInit, 0);
+  std::vector<int32_t> ord((size_t)epochs * N);
+  host_epoch_orders((int)N, seed, epochs, ord.data());
+  DevMem dphi, dy, dord, dth, dst, dstat, dtb;
+  HIPCHK(dphi.alloc(8 * (size_t)n * N));
+  HIPCHK(dy.alloc(8 * (size_t)N));
+  HIPCHK(dord.alloc(4 * ord.size()));
+  HIPCHK(dth.alloc(8 * (size_t)n));
+  HIPCHK(dst.alloc(8 * (size_t)n * total));
+  HIPCHK(dstat.alloc(4));
+  HIPCHK(dtb.alloc(8));
+  HIPCHK(hipMemcpy(dphi.p, phi, 8 * (size_t)n * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy.p, y, 8 * (size_t)N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dord.p, ord.data(), 4 * ord.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dth.p, th0.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(dstat.p, 0, 4));
+  HIPCHK(hipMemset(dtb.p, 0, 8));
+  for (long long t = 0; t < total; ++t) {
+    hipError_t e = launch_gpnt(dphi.as<double>(), dy.as<double>(), dord.as<int32_t>(), (int)n, (int)N,
+                               (int)m, (int)nb, total, signal_var, sigma_theta, eps_theta, decay_rate,
+                               seed, dth.as<double>(), dst.as<double>(), dstat.as<int32_t>(),
+                               dtb.as<long long>(), (int)t, nullptr);
+    if (e != hipSuccess) return hip_fail(e, "gpnt kernel");
+  }
+  int32_t st = 0;
+  HIPCHK(hipMemcpy(&st, dstat.p, 4, hipMemcpyDeviceToHost));
+  if (st) {
+    std::memset(theta_store, 0, 8 * (size_t)n * total);
+    set_error("Get NaN in theta. Try smaller epsilon");
+    return GPT_ERR_NAN_THETA;
+  }
+  HIPCHK(hipMemcpy(theta_store, dst.p, 8 * (size_t)n * total, hipMemcpyDeviceToHost));
+  return GPT_OK;
+}

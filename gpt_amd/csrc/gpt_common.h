@@ -1,0 +1,49 @@
+// Shared device/host helpers for libgptsgld: Philox4x32-10 streams, wave reductions.
+//
+// The Philox stream layout is the framework's RNG contract (see oracle/philox.py for the
+// table).  It replaces Julia's global MersenneTwister draws at GPT_SGLD.jl:357-420; the
+// consumption points are the reference's, the bits are ours.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GPT_HD __host__ __device__ __forceinline__
+
+namespace gpt {
+
+enum Stream : uint32_t {
+  kWInit = 1, kUInit = 2, kPerm = 3, kWNoise = 4, kUNoise = 5,
+  kThetaInit = 6, kThetaNoise = 7, kSampleNZ = 8, kFeatZ = 9, kFeatB = 10
+};
+
+struct U4 { uint32_t x, y, z, w; };
+
+GPT_HD U4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_t seed) {
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+GPT_HD double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6) + 0.5) * (1.0 / 9007199254740992.0);
+}
+
+// Element e of normal stream (c1, c2, c3): Box–Muller on the block at c0 = e>>1.
+GPT_HD double normal_at(uint64_t seed, uint32_t e, uint32_t c1, uint32_t c2, uint32_t c3) {
+  const U4 x = philox4x32(e >> 1, c1, c2, c3, seed);
+  const double u1 = u53(x.x, x.y), u2 = u53(x.z, x.w);
+  const double rad = sqrt(-2.0 * log(u1));
+  const double th = 6.283185307179586 * u2;   // 2π·u2 (2.0*np.pi*u2 in the oracle)
+  return (e & 1u) ? rad * sin(th) : rad * cos(th);
+}
+
+}  // namespace gpt

@@ -1,0 +1,107 @@
+// Internal declarations shared by the libgptsgld translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+#include "gpt_common.h"
+#include "../../include/gptsgld.h"
+
+namespace gpt {
+
+constexpr int kNT = 512;           // threads per workgroup (8 waves of 64)
+constexpr int kNW = kNT / 64;      // waves per workgroup
+constexpr int kDMax = 16;          // max input dimensions D handled by the kernels
+
+// Per-chain device state.  All pointers are device pointers.
+struct ChainDesc {
+  const double* phi;     // n*D*N   training features, Julia layout
+  const double* y;       // N       training targets
+  const int32_t* order;  // E*N     cumulative epoch orders (0-based rows), see host
+  double* w;             // 2*Q     ping-pong: w_t at (t&1)*Q
+  double* U;             // n*r*D   current Stiefel factors (block k owns slice k)
+  double* temp;          // 2*D*r*m ping-pong temp[k,l,i] of the NEXT batch
+  double* w_store;       // Q*nstore or nullptr
+  double* U_store;       // n*r*D*nstore or nullptr
+  double* diag;          // (1+D)*steps per-step gradient norms or nullptr
+  int32_t* status;       // 0 ok, 1 NaN in geodesic
+  uint64_t seed;
+};
+
+struct StepParams {
+  int n, D, N, r, Q, m, nb;       // nb = numbatches = ceil(N/m)
+  int burnin_steps;               // burnin*nb
+  long long total_steps;
+  int store_every;
+  int langevin, stiefel;
+  double signal_var, sigma_w, epsw, epsU;
+  const int32_t* I0;              // Q*D 0-based, layout q + Q*k
+};
+
+GPT_HD size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// LDS carve of the step kernel (bytes).  Shared by host (size) and device (offsets).
+struct StepLayout {
+  int MP, NP;
+  size_t o_temp, o_I, o_w, o_idx, o_y, o_res, o_coef, o_red, o_U, o_W, o_small, bytes;
+  int small_stride;  // doubles per expm scratch matrix
+};
+
+GPT_HD StepLayout step_layout(int n, int D, int r, int Q, int m) {
+  StepLayout L;
+  L.MP = ((m + 7) / 8) * 8 + 1;   // odd (bank spread) and covers the 8-wide unrolled reads
+  L.NP = ((n + 63) / 64) * 64;
+  size_t o = 0;
+  L.o_temp = o; o = al16(o + 8 * (size_t)D * r * L.MP);
+  L.o_I = o;    o = al16(o + 4 * (size_t)Q * D);
+  L.o_w = o;    o = al16(o + 8 * (size_t)Q);
+  L.o_idx = o;  o = al16(o + 4 * (size_t)m);
+  L.o_y = o;    o = al16(o + 8 * (size_t)m);
+  L.o_res = o;  o = al16(o + 8 * (size_t)m);
+  L.o_coef = o; o = al16(o + 8 * (size_t)r * L.MP);
+  L.o_red = o;  o = al16(o + 8 * (size_t)kNW * (1 + r) * 64);
+  L.o_U = o;    o = al16(o + 8 * (size_t)r * L.NP);
+  L.o_W = o;    o = al16(o + 8 * (size_t)r * L.NP);
+  L.o_small = o;
+  const int nn = 2 * r;
+  L.small_stride = nn * nn;
+  // grams (3 r^2) + norms (r) + flag(2) + wave-0 expm scratch (9 nn^2) + wave-1 (9 nn^2)
+  o = al16(o + 8 * (size_t)(3 * r * r + r + 2 + 18 * nn * nn));
+  L.bytes = o;
+  return L;
+}
+
+// Host helpers (capi.hip / sgld.hip)
+void set_error(const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+// Launch wrappers implemented in sgld.hip / pred.hip / feature.hip
+hipError_t launch_temp_init(const StepParams& P, const ChainDesc* chains, int nchains,
+                            const long long* tbase, hipStream_t st);
+hipError_t launch_step(const StepParams& P, const ChainDesc* chains, int nchains,
+                       const long long* tbase, int t_local, hipStream_t st);
+hipError_t launch_advance(long long* tbase, long long by, hipStream_t st);
+bool rank_supported(int r);
+
+hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, const double* phitest,
+                       int n, int D, long long Ntest, int r, int Q, int S, double* fhat,
+                       hipStream_t st);
+hipError_t launch_mean_rmse(const double* fhat, const double* ytest, long long Ntest, int S,
+                            double* mean_out, double* sse_out, hipStream_t st);
+hipError_t launch_feature(const double* X, long long N, int D, const double* ls, double c,
+                          const double* Z, const double* b, int n, double* phi, hipStream_t st);
+hipError_t launch_feature_notensor(const double* X, long long N, int D, const double* ls,
+                                   double c, const double* Z, const double* b, int n,
+                                   double* phi, hipStream_t st);
+hipError_t launch_gpnt(const double* phi, const double* y, const int32_t* order, int n, int N,
+                       int m, int nb, long long total, double signal_var, double sigma_theta,
+                       double eps_theta, double decay_rate, uint64_t seed, double* theta,
+                       double* theta_store, int32_t* status, const long long* tbase, int t_local,
+                       hipStream_t st);
+
+// Host-side Philox consumers (init / permutations / samplenz)
+void host_init_state(int n, int r, int D, int Q, uint64_t seed, bool stiefel, double sigma_w,
+                     double* w, double* U);
+void host_epoch_orders(int N, uint64_t seed, int epochs, int32_t* out);  // E*N cumulative
+
+}  // namespace gpt

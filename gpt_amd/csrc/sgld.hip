@@ -1,0 +1,397 @@
+// Fused tensor-GP SGLD step for MI355X (gfx950).
+//
+// One launch = one SGLD step (GPT_SGLD.jl:377-445) of every chain.  Grid (D+1, chains):
+//   block k < D : owns U^(k) (n×r, in LDS).  Recomputes V/fhat/residual (cheap, identical in
+//                 every block), forms A[:,k,:] without the division of computeU_phi, streams
+//                 phi[:,k,batch] once for gradU^(k) (Psi is never materialised), does the
+//                 Stiefel projection + geodesic (two Padé expm on two waves), writes U^(k),
+//                 and — fused — streams phi[:,k,next batch] to produce temp[k,:,:] of the NEXT
+//                 step with the new U^(k).
+//   block D     : owns w: gradw from V and the residual, the Langevin update and w_store.
+// The only grid-wide dependency of a step (every block needs temp of all k) is carried by the
+// kernel boundary; temp/w are ping-ponged by step parity.  The host captures an epoch of
+// launches in a hipGraph.
+#include "device_util.h"
+
+namespace gpt {
+
+template <int R>
+__global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
+                                                        const ChainDesc* __restrict__ chains,
+                                                        const long long* __restrict__ tbase,
+                                                        int t_local) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const ChainDesc C = chains[blockIdx.y];
+  const int k = blockIdx.x;
+  const int tid = threadIdx.x, wv = tid >> 6;
+  const long long t = tbase[0] + t_local;
+  if (t >= P.total_steps) return;
+  if (__hip_atomic_load(C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+
+  const int n = P.n, D = P.D, Q = P.Q, m = P.m;
+  const StepLayout L = step_layout(n, D, R, Q, m);
+  const int MP = L.MP, NP = L.NP;
+  double* temp_l = (double*)(smem + L.o_temp);
+  int* I_l = (int*)(smem + L.o_I);
+  double* w_l = (double*)(smem + L.o_w);
+  int* idx_l = (int*)(smem + L.o_idx);
+  double* y_l = (double*)(smem + L.o_y);
+  double* res_l = (double*)(smem + L.o_res);
+  double* coef_l = (double*)(smem + L.o_coef);
+  double* red = (double*)(smem + L.o_red);
+  double* U_l = (double*)(smem + L.o_U);
+  double* W_l = (double*)(smem + L.o_W);
+  double* sm = (double*)(smem + L.o_small);
+
+  const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
+  const int start = b * m;
+  const int Bt = min(m, P.N - start);
+  const int32_t* ord = C.order + (size_t)e * P.N + start;
+  const bool wblock = (k == D);
+
+  // ---- P0: stage temp (this batch), I, w, batch rows/targets, U^(k)
+  {
+    const double* tsrc = C.temp + (size_t)(t & 1) * D * R * m;
+    for (int o = tid; o < D * R * m; o += kNT) {
+      const int row = o / m, i = o - row * m;
+      temp_l[row * MP + i] = tsrc[o];
+    }
+    for (int o = tid; o < Q * D; o += kNT) {
+      const int q = o / D, kk = o - q * D;
+      I_l[o] = P.I0[q + Q * kk];
+    }
+    const double* wsrc = C.w + (size_t)(t & 1) * Q;
+    for (int q = tid; q < Q; q += kNT) w_l[q] = wsrc[q];
+    for (int i = tid; i < Bt; i += kNT) {
+      const int row = ord[i];
+      idx_l[i] = row;
+      y_l[i] = C.y[row];
+    }
+    for (int o = tid; o < R * MP; o += kNT) coef_l[o] = 0.0;
+    if (!wblock) {
+      const double* Uk = C.U + (size_t)n * R * k;
+      for (int o = tid; o < R * NP; o += kNT) {
+        const int l = o / NP, j = o - l * NP;
+        U_l[o] = j < n ? Uk[j + (size_t)n * l] : 0.0;
+        W_l[o] = 0.0;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- P1: V, fhat, residual, A[:,k,:] (GPT_SGLD.jl:384-399)
+  const int kown = wblock ? -1 : k;
+  const double cN = (double)P.N / (double)Bt;
+  for (int ic = 0; ic < Bt; ic += 64) {
+    vphase_partials<R>(temp_l, MP, I_l, w_l, Q, D, kown, ic, Bt, red);
+    __syncthreads();
+    const int ncomp = wblock ? 1 : (1 + R);
+    for (int o = tid; o < ncomp * 64; o += kNT) {
+      const int comp = o >> 6, ln = o & 63, i = ic + ln;
+      double s = 0.0;
+#pragma unroll
+      for (int w2 = 0; w2 < kNW; ++w2) s += red[(w2 * (1 + R) + comp) * 64 + ln];
+      if (i < Bt) {
+        if (comp == 0) res_l[i] = y_l[i] - s;
+        else coef_l[(comp - 1) * MP + i] = s;
+      }
+    }
+    __syncthreads();
+  }
+
+  const long long post = t - P.burnin_steps;
+  const bool store = post >= 0 && ((post + 1) % P.store_every) == 0;
+  const long long slot = store ? (post + 1) / P.store_every - 1 : 0;
+
+  if (wblock) {
+    // ---- gradw and the Langevin step on w (GPT_SGLD.jl:393, 411-414)
+    double gn2 = 0.0;
+    const double inv_sw2 = 1.0 / (P.sigma_w * P.sigma_w);
+    const double sqe = sqrt(P.epsw);
+    for (int q = tid; q < Q; q += kNT) {
+      int Iq[kDMax];
+#pragma unroll
+      for (int kk = 0; kk < kDMax; ++kk) Iq[kk] = kk < D ? I_l[q * D + kk] : 0;
+      double g = 0.0;
+      for (int i = 0; i < Bt; ++i) {
+        double v = 1.0;
+#pragma unroll
+        for (int kk = 0; kk < kDMax; ++kk)
+          if (kk < D) v *= temp_l[(kk * R + Iq[kk]) * MP + i];
+        g = fma(v, res_l[i], g);
+      }
+      const double wq = w_l[q];
+      const double gradw = cN * g / P.signal_var - wq * inv_sw2;
+      double step = P.epsw * gradw / 2;
+      if (P.langevin) step += sqe * normal_at(C.seed, (uint32_t)q, (uint32_t)t, kWNoise, 0);
+      const double wn = wq + step;
+      C.w[(size_t)((t + 1) & 1) * Q + q] = wn;
+      if (store && C.w_store) C.w_store[(size_t)slot * Q + q] = wn;
+      gn2 = fma(gradw, gradw, gn2);
+    }
+    if (C.diag) {
+      const double tot = blk_sum(gn2, red);
+      if (tid == 0) C.diag[(size_t)t * (1 + D)] = sqrt(tot);
+    }
+    return;
+  }
+
+  // coef[l][i] = A[l][i]·res[i]
+  for (int o = tid; o < R * Bt; o += kNT) {
+    const int l = o / Bt, i = o - l * Bt;
+    coef_l[l * MP + i] *= res_l[i];
+  }
+  __syncthreads();
+
+  // ---- P2: gradU^(k) = (N/B)/σ² Σ_i phi[:,k,i] (A[:,k,i] res_i)ᵀ   (GPT_SGLD.jl:396-408)
+  const double cU = cN / P.signal_var;
+  const double sq = sqrt(P.epsU);
+  const long long koff = (long long)n * k, rstride = (long long)n * D;
+  double gn2 = 0.0;
+  for (int j = tid; j < n; j += kNT) {
+    double acc[R];
+#pragma unroll
+    for (int l = 0; l < R; ++l) acc[l] = 0.0;
+    for (int i0 = 0; i0 < Bt; i0 += 8) {
+      double p[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = min(i0 + u, Bt - 1);
+        p[u] = C.phi[koff + (long long)uni(idx_l[i]) * rstride + j];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int l = 0; l < R; ++l) acc[l] = fma(p[u], coef_l[l * MP + i0 + u], acc[l]);
+    }
+#pragma unroll
+    for (int l = 0; l < R; ++l) {
+      const double G = acc[l] * cU;
+      gn2 = fma(G, G, gn2);
+      const double xi = P.langevin
+          ? normal_at(C.seed, (uint32_t)(j + n * l), (uint32_t)t, kUNoise, (uint32_t)k) : 0.0;
+      if (P.stiefel) {
+        W_l[l * NP + j] = sq * G / 2 + xi;                      // :420 drive
+      } else {                                                   // :426 / :437
+        const double u = U_l[l * NP + j];
+        U_l[l * NP + j] = u + (P.epsU * (G - n * u) / 2 + sq * xi);
+      }
+    }
+  }
+  if (C.diag) {
+    const double tot = blk_sum(gn2, red);
+    if (tid == 0) C.diag[(size_t)t * (1 + D) + 1 + k] = sqrt(tot);
+  }
+  __syncthreads();
+
+  if (P.stiefel) {
+    double* Mg = sm;              // r×r   Uᵀ·drive
+    double* Ag = sm + R * R;      // r×r   Uᵀ·mom
+    double* Sg = sm + 2 * R * R;  // r×r   momᵀ·mom
+    double* nrm = sm + 3 * R * R; // r
+    int* flag = (int*)(sm + 3 * R * R + R);
+    double* X0 = sm + 3 * R * R + R + 2;       // wave-0 expm region (9·(2r)² doubles)
+    double* X1 = X0 + 9 * (4 * R * R);         // wave-1 expm region
+    // ---- proj (GPT_SGLD.jl:14-16): mom = V − U(UᵀV + VᵀU)/2
+    blk_gram<R>(U_l, W_l, NP, n, 0, Mg, red);
+    for (int j = tid; j < n; j += kNT) {
+      double vj[R], uj[R];
+#pragma unroll
+      for (int l = 0; l < R; ++l) { vj[l] = W_l[l * NP + j]; uj[l] = U_l[l * NP + j]; }
+#pragma unroll
+      for (int bb = 0; bb < R; ++bb) {
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a < R; ++a) s = fma(uj[a], Mg[a * R + bb] + Mg[bb * R + a], s);
+        W_l[bb * NP + j] = vj[bb] - s / 2;
+      }
+    }
+    __syncthreads();
+    // ---- geod (GPT_SGLD.jl:19-37)
+    blk_gram<R>(U_l, W_l, NP, n, 1, Ag, red);   // Ag, then Sg right after it
+    const double tt = sq;
+    const int nn = 2 * R;
+    if (wv == 0) {
+      for (int o = tid; o < nn * nn; o += 64) {
+        const int i = o / nn, j = o - i * nn;
+        double v;
+        if (i < R) v = j < R ? Ag[i * R + j] : -Sg[i * R + (j - R)];
+        else v = j < R ? (i - R == j ? 1.0 : 0.0) : Ag[(i - R) * R + (j - R)];
+        X0[o] = tt * v;
+      }
+      wave_sync();
+      const bool bad = wave_expm(X0, nn);
+      if (tid == 0) flag[0] = bad ? 1 : 0;
+    } else if (wv == 1) {
+      const int ln = tid - 64;
+      for (int o = ln; o < R * R; o += 64) X1[o] = -tt * Ag[o];
+      wave_sync();
+      wave_expm(X1, R);
+    }
+    __syncthreads();
+    if (flag[0]) {
+      if (tid == 0) __hip_atomic_store(C.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    const double* E = X0 + 8 * nn * nn;     // 2r×2r, use columns 0..r-1
+    const double* mexp = X1 + 8 * R * R;    // r×r
+    for (int j = tid; j < n; j += kNT) {
+      double x[2 * R];
+#pragma unroll
+      for (int l = 0; l < R; ++l) { x[l] = U_l[l * NP + j]; x[R + l] = W_l[l * NP + j]; }
+      double row1[R];
+#pragma unroll
+      for (int l = 0; l < R; ++l) {
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a < 2 * R; ++a) s = fma(x[a], E[a * nn + l], s);
+        row1[l] = s;
+      }
+#pragma unroll
+      for (int l = 0; l < R; ++l) {
+        double s = 0.0;
+#pragma unroll
+        for (int c2 = 0; c2 < R; ++c2) s = fma(row1[c2], mexp[c2 * R + l], s);
+        W_l[l * NP + j] = s;
+      }
+    }
+    __syncthreads();
+    blk_gram<R>(W_l, W_l, NP, n, 2, nrm, red);
+    for (int o = tid; o < R * n; o += kNT) {
+      const int l = o / n, j = o - l * n;
+      U_l[l * NP + j] = W_l[l * NP + j] / sqrt(nrm[l]);
+    }
+    __syncthreads();
+  }
+
+  // ---- write U^(k) (and the sample store, GPT_SGLD.jl:441-444)
+  {
+    double* Uk = C.U + (size_t)n * R * k;
+    double* Us = (store && C.U_store) ? C.U_store + ((size_t)slot * D + k) * n * R : nullptr;
+    for (int o = tid; o < R * n; o += kNT) {
+      const int l = o / n, j = o - l * n;
+      const double u = U_l[l * NP + j];
+      Uk[o] = u;
+      if (Us) Us[o] = u;
+    }
+  }
+
+  // ---- P5: temp[k,:,:] of the next step with the new U^(k) (phidotU, GPT_SGLD.jl:193-205)
+  const long long t1 = t + 1;
+  if (t1 < P.total_steps) {
+    const int e1 = (int)(t1 / P.nb), b1 = (int)(t1 - (long long)e1 * P.nb);
+    const int s1 = b1 * m;
+    const int B1 = min(m, P.N - s1);
+    const int32_t* ord1 = C.order + (size_t)e1 * P.N + s1;
+    for (int i = tid; i < B1; i += kNT) idx_l[i] = ord1[i];
+    __syncthreads();
+    double* tdst = C.temp + (size_t)(t1 & 1) * D * R * m + (size_t)k * R * m;
+    phidotU_tile<R>(C.phi, koff, rstride, idx_l, B1, n, NP, U_l,
+                    [&](int l, int i, double v) { tdst[l * m + i] = v; });
+  }
+}
+
+// temp of the first step of a run (or after a restart): phidotU of batch t with U as stored.
+template <int R>
+__global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
+                                                        const ChainDesc* __restrict__ chains,
+                                                        const long long* __restrict__ tbase) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const ChainDesc C = chains[blockIdx.y];
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const long long t = tbase[0];
+  if (t >= P.total_steps) return;
+  const int n = P.n, D = P.D, m = P.m;
+  const StepLayout L = step_layout(n, D, R, P.Q, m);
+  const int NP = L.NP;
+  int* idx_l = (int*)(smem + L.o_idx);
+  double* U_l = (double*)(smem + L.o_U);
+  const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
+  const int start = b * m;
+  const int Bt = min(m, P.N - start);
+  const int32_t* ord = C.order + (size_t)e * P.N + start;
+  for (int i = tid; i < Bt; i += kNT) idx_l[i] = ord[i];
+  const double* Uk = C.U + (size_t)n * R * k;
+  for (int o = tid; o < R * NP; o += kNT) {
+    const int l = o / NP, j = o - l * NP;
+    U_l[o] = j < n ? Uk[j + (size_t)n * l] : 0.0;
+  }
+  __syncthreads();
+  double* tdst = C.temp + (size_t)(t & 1) * D * R * m + (size_t)k * R * m;
+  phidotU_tile<R>(C.phi, (long long)n * k, (long long)n * D, idx_l, Bt, n, NP, U_l,
+                  [&](int l, int i, double v) { tdst[l * m + i] = v; });
+}
+
+__global__ void advance_kernel(long long* tbase, long long by) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) tbase[0] += by;
+}
+
+#define GPT_RANKS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(15) X(16) X(20)
+
+bool rank_supported(int r) {
+  switch (r) {
+#define CASE(RR) case RR:
+    GPT_RANKS(CASE)
+#undef CASE
+    return true;
+    default: return false;
+  }
+}
+
+hipError_t launch_temp_init(const StepParams& P, const ChainDesc* chains, int nchains,
+                            const long long* tbase, hipStream_t st) {
+  const StepLayout L = step_layout(P.n, P.D, P.r, P.Q, P.m);
+  dim3 grid(P.D, nchains);
+  switch (P.r) {
+#define CASE(RR)                                                                           \
+  case RR:                                                                                 \
+    hipLaunchKernelGGL(temp_init_kernel<RR>, grid, dim3(kNT), L.bytes, st, P, chains, tbase); \
+    break;
+    GPT_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_step(const StepParams& P, const ChainDesc* chains, int nchains,
+                       const long long* tbase, int t_local, hipStream_t st) {
+  const StepLayout L = step_layout(P.n, P.D, P.r, P.Q, P.m);
+  dim3 grid(P.D + 1, nchains);
+  switch (P.r) {
+#define CASE(RR)                                                                              \
+  case RR:                                                                                    \
+    hipLaunchKernelGGL(sgld_step_kernel<RR>, grid, dim3(kNT), L.bytes, st, P, chains, tbase,  \
+                       t_local);                                                              \
+    break;
+    GPT_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_advance(long long* tbase, long long by, hipStream_t st) {
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, st, tbase, by);
+  return hipGetLastError();
+}
+
+// Opt the kernels into >64 KiB of dynamic LDS once per process.
+hipError_t set_lds_limits() {
+  static bool done = false;
+  if (done) return hipSuccess;
+  hipError_t e = hipSuccess;
+#define CASE(RR)                                                                              \
+  e = hipFuncSetAttribute((const void*)sgld_step_kernel<RR>,                                   \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);            \
+  if (e != hipSuccess) return e;                                                              \
+  e = hipFuncSetAttribute((const void*)temp_init_kernel<RR>,                                   \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);            \
+  if (e != hipSuccess) return e;
+  GPT_RANKS(CASE)
+#undef CASE
+  done = true;
+  return e;
+}
+
+}  // namespace gpt

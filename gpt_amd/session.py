@@ -1,0 +1,124 @@
+"""Device-resident multi-chain SGLD sessions (the benchmark and multi-GPU path).
+
+Inputs stay in HBM as torch tensors (PyTorch is only the allocator/stream plumbing); every
+chain step runs in libgptsgld.so's fused HIP kernel.  Chains share the configuration and
+may share or own their (phi, y) (a hyper-parameter sweep gives each chain its own phi, as
+kin40kExperiment.jl:67-72 does; posterior chains share one, BASELINE config 4).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import SGLDConfig, check, lib
+from .GPT_SGLD import make_config
+
+
+class SGLDSession:
+    def __init__(self, phis, ys, I, r, Q, m, epsw, epsU, signal_var, burnin, maxepoch, seeds,
+                 sigma_w=1.0, langevin=True, stiefel=True, store_every=1, max_steps=0,
+                 store=True, diag=False, stream=None):
+        import torch
+        if not isinstance(phis, (list, tuple)):
+            phis = [phis]
+        if not isinstance(ys, (list, tuple)):
+            ys = [ys]
+        seeds = list(seeds)
+        nch = len(seeds)
+        if len(phis) == 1 and nch > 1:
+            phis = phis * nch
+        if len(ys) == 1 and nch > 1:
+            ys = ys * nch
+        if len(phis) != nch or len(ys) != nch:
+            raise ValueError("need one (phi, y) per chain or a shared one")
+        for p in phis:
+            if p.dtype != torch.float64 or not p.is_cuda or p.dim() != 3 or not p.is_contiguous():
+                raise ValueError("phi must be a contiguous float64 device tensor of torch shape "
+                                 "(N, D, n) == Julia phi (n, D, N)")
+        N, D, n = phis[0].shape     # torch (N, D, n) row-major == Julia (n, D, N) column-major
+        self._keep = (phis, ys)
+        self.n, self.D, self.N, self.r, self.Q, self.m = int(n), int(D), int(N), r, Q, m
+        self.nchains = nch
+        I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+        self.cfg = make_config(self.n, self.D, self.N, r, Q, m, epsw, epsU, signal_var, sigma_w,
+                               burnin, maxepoch, 0, langevin, stiefel, store_every, max_steps)
+        pp = (C.c_void_p * nch)(*[p.data_ptr() for p in phis])
+        yy = (C.c_void_p * nch)(*[y.data_ptr() for y in ys])
+        sd = (C.c_uint64 * nch)(*[int(s) & (2 ** 64 - 1) for s in seeds])
+        h = C.c_void_p()
+        flags = (1 if store else 0) | (2 if diag else 0)
+        st = C.c_void_p(stream) if stream else None
+        check(lib().gpt_sgld_session_create(C.byref(self.cfg), nch, sd, pp, yy,
+                                            I.ctypes.data_as(_lib.P_I32), flags, st, C.byref(h)))
+        self._h = h
+        self.numbatches = -(-self.N // m)
+        total = (burnin + maxepoch) * self.numbatches
+        self.total_steps = total if max_steps <= 0 else min(total, max_steps)
+        self.nstore = (maxepoch * self.numbatches) // store_every
+
+    def run(self, nsteps):
+        check(lib().gpt_sgld_session_run(self._h, int(nsteps)))
+
+    def time_steps(self, nsteps):
+        """Run nsteps un-captured steps with a hipEvent pair around every step-kernel launch;
+        returns the mean step-kernel duration in microseconds."""
+        avg = C.c_double(0.0)
+        check(lib().gpt_sgld_session_time_steps(self._h, int(nsteps), C.byref(avg)))
+        return avg.value
+
+    def sync(self):
+        check(lib().gpt_sgld_session_sync(self._h))
+
+    @property
+    def steps_done(self):
+        return int(lib().gpt_sgld_session_steps_done(self._h))
+
+    def device_state(self, chain):
+        w = C.c_void_p(); U = C.c_void_p(); ws = C.c_void_p(); Us = C.c_void_p(); ns = C.c_int64()
+        check(lib().gpt_sgld_session_state(self._h, chain, C.byref(w), C.byref(U), C.byref(ws),
+                                           C.byref(Us), C.byref(ns)))
+        return w.value, U.value, ws.value, Us.value, ns.value
+
+    def fetch(self, chain, diag=False):
+        """(w_store, U_store, status[, diag]) of one chain, host numpy in Julia layout."""
+        ws = np.zeros((self.Q, self.nstore), order="F")
+        Us = np.zeros((self.n, self.r, self.D, self.nstore), order="F")
+        dg = np.zeros((1 + self.D, self.total_steps), order="F") if diag else None
+        st = C.c_int32(0)
+        check(lib().gpt_sgld_session_fetch(self._h, chain, ws.ctypes.data_as(_lib.P_D),
+                                           Us.ctypes.data_as(_lib.P_D),
+                                           dg.ctypes.data_as(_lib.P_D) if diag else None,
+                                           C.byref(st)))
+        return (ws, Us, st.value, dg) if diag else (ws, Us, st.value)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().gpt_sgld_session_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def feature_device(X, length_scale, sigma_RBF, phi_scale, Z, b, stream=None):
+    """phi on the device (torch (N, D, n) == Julia (n, D, N)) from device tensors X (N, D)
+    [Julia column-major => torch (D, N)], Z/b (n, D) [torch (D, n)], length_scale (D,)."""
+    import torch
+    D, N = X.shape
+    n = Z.shape[1]
+    phi = torch.empty((N, D, n), dtype=torch.float64, device=X.device)
+    check(lib().gpt_feature_dev(C.c_void_p(X.data_ptr()), N, D, C.c_void_p(length_scale.data_ptr()),
+                                D, float(sigma_RBF), float(phi_scale), C.c_void_p(Z.data_ptr()),
+                                C.c_void_p(b.data_ptr()), n, C.c_void_p(phi.data_ptr()),
+                                C.c_void_p(stream) if stream else None))
+    return phi
+
+
+def pred_device(w_ptr, U_ptr, I0_dev, phitest, n, D, Ntest, r, Q, S, fhat_out, stream=None):
+    """fhat (Ntest, S) on the device from S consecutive samples at w_ptr / U_ptr."""
+    check(lib().gpt_pred_dev(C.c_void_p(w_ptr), C.c_void_p(U_ptr), C.c_void_p(I0_dev.data_ptr()),
+                             C.c_void_p(phitest.data_ptr()), n, D, Ntest, r, Q, S,
+                             C.c_void_p(fhat_out.data_ptr()), C.c_void_p(stream) if stream else None))

@@ -1,0 +1,138 @@
+/* gptsgld.h — C ABI of libgptsgld.so, the MI355X-native tensor-GP SGLD path.
+ *
+ * Drop-in boundary for the Julia module API that the reference's experiment scripts import
+ * with `@everywhere using GPT_SGLD` (kin40kExperiment.jl:3).  Each entry point below names
+ * the reference function it replaces (file:line under hyunjik11/GPT).  INTEGRATION.md shows
+ * the Julia `ccall` shim and the Python ctypes binding.
+ *
+ * Conventions:
+ *  - Arrays are Julia column-major: phi[j,k,i] at j + n*(k + D*i); U[j,l,k] at j + n*(l + r*k);
+ *    I[q,k] (Int32, 1-based, values 1..r) at q + Q*k; X[i,k] at i + N*k; Float64 everywhere.
+ *  - The caller allocates every output (zero-copy with `ccall(..., Ptr{Float64})`).  The
+ *    library owns only device scratch.
+ *  - Return value: GPT_OK, or an error code; gpt_last_error() has a thread-local message.
+ *    GPT_ERR_NAN_GEODESIC mirrors GPT_SGLD.jl:23-26,422-424: the sample stores are zero-filled.
+ *  - Host-pointer entry points copy to the device, run, and copy back (PCIe included).
+ *    The *_dev entry points take device pointers and a hipStream_t (as void*) and are what the
+ *    benchmark times (inputs resident in HBM).
+ *  - Reentrant: no global state except the per-thread error string.
+ */
+#ifndef GPTSGLD_H
+#define GPTSGLD_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPT_OK 0
+#define GPT_ERR_NAN_GEODESIC 1
+#define GPT_ERR_BAD_DIMS 2
+#define GPT_ERR_HIP 3
+#define GPT_ERR_NAN_THETA 4
+
+/* Sampler configuration: the scalar arguments of GPTregression (GPT_SGLD.jl:345) plus the
+ * framework's store policy.  sigma_w = 1 is Generation C/D (GPT_SGLD.jl:354); Generation A/B
+ * (GPT_SGLDERM, GPT_SGLD_p.jl:155) passes sigma_w = sqrt(n^D/Q) and signal_var = sigma^2. */
+typedef struct gpt_sgld_config {
+  int64_t n;          /* random features per input dimension (reference `n`)            */
+  int64_t D;          /* input dimensions                                               */
+  int64_t N;          /* training rows                                                  */
+  int64_t r;          /* Stiefel rank                                                   */
+  int64_t Q;          /* non-zeros of the sparse Tucker core                            */
+  int64_t m;          /* minibatch size (reference `m`)                                 */
+  double epsw, epsU;  /* SGLD step sizes                                                */
+  double signal_var;  /* observation noise variance                                     */
+  double sigma_w;     /* prior s.d. of w                                                */
+  int64_t burnin, maxepoch;
+  uint64_t seed;      /* param_seed: Philox key of every draw of this chain             */
+  int32_t langevin;   /* 1 = SGLD (noise), 0 = SGD                                      */
+  int32_t stiefel;    /* 1 = geodesic Stiefel update, 0 = Euclidean update of U         */
+  int64_t store_every;/* 1 = reference (every post-burn-in step); numbatches = epoch ends */
+  int64_t max_steps;  /* 0 = run all (burnin+maxepoch)*numbatches steps                  */
+} gpt_sgld_config;
+
+/* ---- features ------------------------------------------------------------------------ */
+/* feature(X,length_scale,sigma_RBF,phi_scale,Z,b)  GPT_SGLD.jl:71-84  -> phi (n,D,N) */
+int gpt_feature(const double* X, int64_t N, int64_t D, const double* length_scale,
+                int64_t ls_len, double sigma_rbf, double phi_scale, const double* Z,
+                const double* b, int64_t n, double* phi_out);
+/* featureNotensor(X,length_scale,sigma_RBF,Z,b)  GPT_SGLD.jl:109-120  -> phi (n,N) */
+int gpt_feature_notensor(const double* X, int64_t N, int64_t D, const double* length_scale,
+                         int64_t ls_len, double sigma_rbf, const double* Z, const double* b,
+                         int64_t n, double* phi_out);
+/* Device form of gpt_feature (all pointers device, hip_stream may be NULL). */
+int gpt_feature_dev(const double* X_dev, int64_t N, int64_t D, const double* ls_dev,
+                    int64_t ls_len, double sigma_rbf, double phi_scale, const double* Z_dev,
+                    const double* b_dev, int64_t n, double* phi_dev, void* hip_stream);
+/* seeded Generation-C inputs of feature(X,n,ls,σ,seed,scale): Z=randn(n,D), b=2π·rand(n,D) */
+int gpt_feature_inputs(int64_t n, int64_t D, uint64_t seed, double* Z_out, double* b_out);
+
+/* samplenz(r,D,Q,seed)  GPT_SGLD.jl:181-190 / GPT_SGLD_p.jl:57-67  -> I (Q,D) Int32 1-based */
+int gpt_samplenz(int64_t r, int64_t D, int64_t Q, uint64_t seed, int32_t* I_out);
+
+/* Initial state of GPTregression (GPT_SGLD.jl:357-369): w (Q), U (n,r,D). */
+int gpt_sgld_init(const gpt_sgld_config* cfg, double* w_out, double* U_out);
+
+/* ---- sampler ------------------------------------------------------------------------- */
+/* GPTregression(phi,y,signal_var,I,r,Q,m,epsw,epsU,burnin,maxepoch,param_seed;langevin,stiefel)
+ * GPT_SGLD.jl:345-448 (also GPT_SGLDERM, GPT_SGLD_p.jl:146-243, via sigma_w/signal_var).
+ * w_init/U_init: NULL = draw from the seed (the reference's srand(param_seed) path).
+ * w_store (Q,T), U_store (n,r,D,T) with T = maxepoch*numbatches/store_every.
+ * diag (nullable): per step [‖gradw‖, ‖gradU_1‖ … ‖gradU_D‖] ((1+D) x steps). */
+int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi, const double* y,
+                        const int32_t* I, const double* w_init, const double* U_init,
+                        double* w_store, double* U_store, double* diag);
+
+/* Multi-chain, device-resident session (benchmark / multi-GPU path).  Chains share the
+ * config except seed; chain c reads phi_dev[c], y_dev[c] (device pointers; may alias). */
+typedef struct gpt_sgld_session gpt_sgld_session;
+int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchains, const uint64_t* seeds,
+                            const double* const* phi_dev, const double* const* y_dev,
+                            const int32_t* I_host, int32_t store_on_device, void* hip_stream,
+                            gpt_sgld_session** out);
+/* Queue `nsteps` SGLD steps of every chain on the session stream (asynchronous). */
+int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps);
+int gpt_sgld_session_sync(gpt_sgld_session* s);
+/* Device pointers of chain c's current state and stores (for pred / collectives). */
+int gpt_sgld_session_state(gpt_sgld_session* s, int32_t chain, double** w_dev, double** U_dev,
+                           double** w_store_dev, double** U_store_dev, int64_t* nstore);
+int64_t gpt_sgld_session_steps_done(gpt_sgld_session* s);
+/* Run `nsteps` steps WITHOUT graph capture, bracketing every step-kernel launch with hipEvents;
+ * *avg_us = mean step-kernel duration (the roofline's per-launch time).  Synchronises. */
+int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, double* avg_us);
+/* Copy chain c's stores / status back (status: GPT_OK or GPT_ERR_NAN_GEODESIC). */
+int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double* w_store, double* U_store,
+                           double* diag, int32_t* status);
+void gpt_sgld_session_destroy(gpt_sgld_session* s);
+
+/* ---- prediction ---------------------------------------------------------------------- */
+/* pred(w,U,I,phitest)  GPT_SGLD.jl:233-243  -> fhat (Ntest) */
+int gpt_pred(const double* w, const double* U, const int32_t* I, const double* phitest,
+             int64_t n, int64_t D, int64_t Ntest, int64_t r, int64_t Q, double* fhat_out);
+/* Device form over S stored samples: fhat_dev (Ntest,S) = pred of each sample.
+ * I_dev is 0-based Int32 (Q,D). */
+int gpt_pred_dev(const double* w_dev, const double* U_dev, const int32_t* I0_dev,
+                 const double* phitest_dev, int64_t n, int64_t D, int64_t Ntest, int64_t r,
+                 int64_t Q, int64_t S, double* fhat_dev, void* hip_stream);
+/* Posterior-mean prediction over S samples + RMSE (GPT_SGLD_p.jl:124-132,
+ * kin40kExperiment.jl:80-87): mean_out (Ntest), returns rmse*scale in *rmse_out. */
+int gpt_pred_mean(const double* w_store, const double* U_store, const int32_t* I,
+                  const double* phitest, const double* ytest, int64_t n, int64_t D,
+                  int64_t Ntest, int64_t r, int64_t Q, int64_t S, double scale,
+                  double* mean_out, double* rmse_out);
+
+/* ---- full-theta model (config 1) ----------------------------------------------------- */
+/* GPNT_SGLD(phi,y,signal_var,sigma_theta,m,eps_theta,decay_rate,burnin,maxepoch,param_seed)
+ * GPT_SGLD.jl:809-847 -> theta_store (n, (maxepoch+burnin)*numbatches) */
+int gpt_gpnt_sgld(const double* phi, const double* y, int64_t n, int64_t N, double signal_var,
+                  double sigma_theta, int64_t m, double eps_theta, double decay_rate,
+                  int64_t burnin, int64_t maxepoch, uint64_t seed, double* theta_store);
+
+const char* gpt_last_error(void);
+int gpt_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPTSGLD_H */

@@ -1,0 +1,427 @@
+"""CPU oracle: a numpy fp64 restatement of the reference tensor-GP SGLD path.
+
+TEST INFRASTRUCTURE — NOT PRODUCT CODE.  Only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import this module.  The product path
+(``gpt_amd`` + ``libgptsgld.so``) never imports, links or executes anything under
+``oracle/``.
+
+Every function restates the Julia reference line for line (citations are
+``/root/reference/<file>:<line>``).  Arrays use Julia's column-major semantics: a Julia
+``phi[j,k,i]`` is ``phi[j, k, i]`` here with ``order='F'`` storage, ``I`` is 1-based
+Int32 exactly as ``samplenz`` returns it.
+
+Randomness: the reference draws from Julia's global MersenneTwister, which cannot be
+reproduced without Julia.  All draws here come from the Philox streams of
+``oracle/philox.py`` (the same contract the HIP kernels implement), consumed at the same
+points in the same order as the reference.  Pinning: ``pred``/``phidotU``/
+``computeV``/``computefhat`` and the column-major layouts are pinned by the reference's
+own fixtures ``TensorSynthData{5D,10D}100N.h5`` (tests/golden); the gradients by the
+finite-difference method of ``Diagnostic_gradients.jl:131-158``; ``expm`` by the Padé
+algorithm of Julia Base 0.3 ``expm!`` (cross-checked against scipy); RNG-dependent
+trajectories are parity-unpinned against Julia and pinned against this oracle.
+"""
+import math
+import numpy as np
+
+from . import philox as px
+
+
+# --------------------------------------------------------------------------- data prep
+def datawhitening(X):
+    """GPT_SGLD.jl:62-67 — centre each column and divide by its (n-1) std."""
+    X = np.array(X, dtype=np.float64, copy=True)
+    if X.ndim == 1:
+        return (X - X.mean()) / X.std(ddof=1)
+    for i in range(X.shape[1]):
+        X[:, i] = (X[:, i] - X[:, i].mean()) / X[:, i].std(ddof=1)
+    return X
+
+
+# --------------------------------------------------------------------------- features
+def feature(X, length_scale, sigma_RBF, phi_scale, Z, b):
+    """GPT_SGLD.jl:71-84.  phi[j,k,i] = c·cos(X[i,k]·Zt[j,k] + b[j,k]),
+    Zt = scale(Z, 1./length_scale), c = phi_scale·σ^(1/D)·sqrt(2/n)."""
+    X = np.asarray(X, dtype=np.float64)
+    N, D = X.shape
+    Z = np.asarray(Z, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64).reshape(Z.shape, order="F")
+    n = Z.shape[0]
+    ls = np.broadcast_to(np.asarray(length_scale, dtype=np.float64), (D,))
+    Zt = Z * (1.0 / ls)[None, :]
+    arg = X.T[None, :, :] * Zt[:, :, None] + b[:, :, None]          # (n, D, N)
+    c = phi_scale * sigma_RBF ** (1.0 / D) * math.sqrt(2.0 / n)
+    return np.asfortranarray(c * np.cos(arg))
+
+
+def featureNotensor(X, length_scale, sigma_RBF, Z, b):
+    """GPT_SGLD.jl:109-120.  phi[j,i] = sqrt(2/n)·σ·cos(Σ_k X[i,k]·Zt[j,k] + b[j])."""
+    X = np.asarray(X, dtype=np.float64)
+    N, D = X.shape
+    Z = np.asarray(Z, dtype=np.float64)
+    n = Z.shape[0]
+    ls = np.broadcast_to(np.asarray(length_scale, dtype=np.float64), (D,))
+    Zt = Z * (1.0 / ls)[None, :]
+    s = np.zeros((n, N))
+    for k in range(D):                       # sum(X[i,:].*Zt[j,:]) left to right
+        s = s + Zt[:, k:k + 1] * X[None, :, k]
+    return np.asfortranarray(math.sqrt(2.0 / n) * sigma_RBF * np.cos(s + np.asarray(b, float).reshape(n, 1)))
+
+
+def seeded_feature_inputs(n, D, seed):
+    """Generation-C seeded ``feature(X,n,ls,σ,seed,scale)``: Z=randn(n,D),
+    b=2π·rand(n,D) drawn from the framework's streams (W_INIT/U_INIT reused with c3 tags)."""
+    Z = px.normals(n * D, seed, 0, 9, 0).reshape((n, D), order="F")
+    x0, x1, _, _ = px.philox4x32(np.arange(n * D, dtype=np.uint32), 0, 10, 0, seed)
+    b = 2.0 * np.pi * px._u53(x0, x1).reshape((n, D), order="F")
+    return Z, b
+
+
+# --------------------------------------------------------------------------- samplenz
+def samplenz_from_L(L, r, D):
+    """GPT_SGLD.jl:181-190 body given the drawn lattice indices L:
+    I[q,:] = digits(L[q], r, D) + 1 (little-endian base-r digits)."""
+    L = np.asarray(L, dtype=np.int64)
+    I = np.empty((len(L), D), dtype=np.int32, order="F")
+    for q, v in enumerate(L):
+        v = int(v)
+        for k in range(D):
+            I[q, k] = v % r + 1
+            v //= r
+    return I
+
+
+def sample_lattice(r, D, Q, seed):
+    """``sample(0:(r^D-1), Q, replace=false)`` restated as a sparse partial Fisher–Yates on
+    the SAMPLENZ stream (c2=8): position i swaps with i + floor(u64·(M-i)/2^64)."""
+    M = int(r) ** int(D)
+    if Q > M:
+        raise ValueError("Q must be <= r^D")
+    x0, x1, _, _ = px.philox4x32(np.arange(Q, dtype=np.uint32), 0, 8, 0, seed)
+    swapped = {}
+    L = []
+    for i in range(Q):
+        u = (int(x0[i]) << 32) | int(x1[i])
+        j = i + ((u * (M - i)) >> 64)
+        vi = swapped.get(i, i)
+        vj = swapped.get(j, j)
+        swapped[i], swapped[j] = vj, vi
+        L.append(vj)
+    return np.array(L, dtype=np.int64)
+
+
+def samplenz(r, D, Q, seed):
+    """Gen-A/C ``samplenz(r,D,Q,seed)`` (GPT_SGLD_p.jl:57-67) on the framework stream."""
+    return samplenz_from_L(sample_lattice(r, D, Q, seed), r, D)
+
+
+# --------------------------------------------------------------------------- forward
+def phidotU(U, phi):
+    """GPT_SGLD.jl:193-205.  temp[k,l,i] = dot(phi[:,k,i], U[:,l,k])."""
+    return np.einsum("jki,jlk->kli", phi, U)
+
+
+def computeV(temp, I):
+    """GPT_SGLD.jl:208-220.  V[q,i] = prod_k temp[k, I[q,k], i] (product in k order)."""
+    Q, D = I.shape
+    V = np.ones((Q, temp.shape[2]))
+    for k in range(D):
+        V = V * temp[k, I[:, k] - 1, :]
+    return V
+
+
+def computefhat(V, w):
+    """GPT_SGLD.jl:223-230.  fhat[i] = dot(V[:,i], w)."""
+    return V.T @ w
+
+
+def pred(w, U, I, phitest):
+    """GPT_SGLD.jl:233-243."""
+    return computefhat(computeV(phidotU(U, phitest), I), w)
+
+
+def computeU_phi(V, temp, I):
+    """GPT_SGLD.jl:246-258.  U_phi[q,i,k] = V[q,i] / temp[k, I[q,k], i]."""
+    Q, D = I.shape
+    out = np.empty((Q, V.shape[1], D))
+    for k in range(D):
+        out[:, :, k] = V / temp[k, I[:, k] - 1, :]
+    return out
+
+
+def computeA(U_phi, w, I, r):
+    """GPT_SGLD.jl:261-273.  A[l,k,i] = sum_{q: I[q,k]=l} U_phi[q,i,k]·w[q]."""
+    Q, B, D = U_phi.shape
+    A = np.zeros((r, D, B))
+    for k in range(D):
+        for l in np.unique(I[:, k]):
+            idx = np.nonzero(I[:, k] == l)[0]
+            A[l - 1, k, :] = w[idx] @ U_phi[idx, :, k]
+    return A
+
+
+def computePsi(A, phi):
+    """GPT_SGLD.jl:276-286.  Psi[:,i,k] = kron(A[:,k,i], phi[:,k,i])."""
+    r, D, B = A.shape
+    n = phi.shape[0]
+    Psi = np.empty((n * r, B, D))
+    for k in range(D):
+        # kron(a, p)[(l)*n + j] = a[l]*p[j]
+        Psi[:, :, k] = (A[:, k, None, :] * phi[None, :, k, :]).reshape(n * r, B)
+    return Psi
+
+
+def gradients(phi_batch, y_batch, w, U, I, N, signal_var, sigma_w=1.0):
+    """GPT_SGLD.jl:384-408: temp, V, fhat, gradw, U_phi, A, Psi, gradU for one minibatch."""
+    n, D, B = phi_batch.shape
+    r = U.shape[1]
+    temp = phidotU(U, phi_batch)
+    V = computeV(temp, I)
+    fhat = computefhat(V, w)
+    res = y_batch - fhat
+    gradw = (N / B) * (V @ res) / signal_var - w / sigma_w ** 2
+    U_phi = computeU_phi(V, temp, I)
+    A = computeA(U_phi, w, I, r)
+    Psi = computePsi(A, phi_batch)
+    gradU = np.empty((n, r, D))
+    for k in range(D):
+        # reshape((N/B)*Psi_k*(y-fhat)/σ², n, r) — Julia column-major reshape
+        gradU[:, :, k] = ((N / B) * (Psi[:, :, k] @ res) / signal_var).reshape((n, r), order="F")
+    return dict(temp=temp, V=V, fhat=fhat, gradw=gradw, A=A, gradU=gradU)
+
+
+def loglik(phi, y, w, U, I, sigma):
+    """Diagnostic_gradients.jl:5-37 — log p(y|x,w,U) (for finite-difference checks)."""
+    fhat = pred(w, U, I, phi)
+    return -np.linalg.norm(y - fhat) ** 2 / (2 * sigma ** 2)
+
+
+# --------------------------------------------------------------------------- Stiefel
+def proj(U, V):
+    """GPT_SGLD.jl:14-16."""
+    return V - U @ (U.T @ V + V.T @ U) / 2
+
+
+_PADE = {
+    3: [120.0, 60.0, 12.0, 1.0],
+    5: [30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0],
+    7: [17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0],
+    9: [17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0,
+        2162160.0, 110880.0, 3960.0, 90.0, 1.0],
+    13: [64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
+         1187353796428800.0, 129060195264000.0, 10559470521600.0, 670442572800.0,
+         33522128640.0, 1323241920.0, 40840800.0, 960960.0, 16380.0, 182.0, 1.0],
+}
+
+
+def expm(A):
+    """Matrix exponential by Padé scaling-and-squaring, restating Julia Base 0.3
+    ``expm!`` (Higham 2005; thresholds 0.015/0.25/0.95/2.1 and 5.4 as in Julia Base,
+    without the LAPACK ``gebal`` balancing step, which does not change the result)."""
+    A = np.array(A, dtype=np.float64)
+    n = A.shape[0]
+    Id = np.eye(n)
+    nA = np.abs(A).sum(axis=0).max() if n else 0.0
+    if not np.isfinite(nA):
+        # Julia's ceil(Int, log2(nA/5.4)) would throw here; the framework takes geod's
+        # NaN bail-out instead (documented in DESIGN.md).
+        return np.full((n, n), np.nan)
+    if nA <= 2.1:
+        if nA > 0.95:
+            C = _PADE[9]
+        elif nA > 0.25:
+            C = _PADE[7]
+        elif nA > 0.015:
+            C = _PADE[5]
+        else:
+            C = _PADE[3]
+        A2 = A @ A
+        P = Id.copy()
+        U = C[1] * P
+        V = C[0] * P
+        for k in range(1, (len(C) - 1) // 2 + 1):
+            k2 = 2 * k
+            P = P @ A2
+            U = U + C[k2 + 1] * P
+            V = V + C[k2] * P
+        U = A @ U
+        X = np.linalg.solve(V - U, V + U)
+    else:
+        s = math.log2(nA / 5.4)
+        si = int(math.ceil(s)) if s > 0 else 0
+        if s > 0:
+            A = A / (2.0 ** si)
+        C = _PADE[13]
+        A2 = A @ A
+        A4 = A2 @ A2
+        A6 = A2 @ A4
+        U = A @ (A6 @ (C[13] * A6 + C[11] * A4 + C[9] * A2)
+                 + C[7] * A6 + C[5] * A4 + C[3] * A2 + C[1] * Id)
+        V = A6 @ (C[12] * A6 + C[10] * A4 + C[8] * A2) + C[6] * A6 + C[4] * A4 + C[2] * A2 + C[0] * Id
+        X = np.linalg.solve(V - U, V + U)
+        for _ in range(si):
+            X = X @ X
+    return X
+
+
+def geod(U, mom, t):
+    """GPT_SGLD.jl:19-37.  Returns (U_new, ok); ok=False reproduces the NaN bail-out
+    (``println`` + ``zeros(n,r)``)."""
+    n, r = U.shape
+    A = U.T @ mom
+    T = np.block([[A, -(mom.T @ mom)], [np.eye(r), A]])
+    with np.errstate(all="ignore"):
+        E = expm(t * T)
+    if np.isnan(E).any():
+        return np.zeros((n, r)), False
+    mexp = expm(-t * A)
+    tmpU = (np.hstack([U, mom]) @ E[:, :r]) @ mexp
+    return tmpU / np.linalg.norm(tmpU, axis=0)[None, :], True
+
+
+def stiefel_init(Zr_n):
+    """GPT_SGLD.jl:365-366: U_k = transpose(sqrtm(Z*Z') \\ Z) = Z'(ZZ')^(-1/2)."""
+    Z = Zr_n
+    evals, evecs = np.linalg.eigh(Z @ Z.T)
+    inv_sqrt = (evecs / np.sqrt(evals)[None, :]) @ evecs.T
+    return Z.T @ inv_sqrt
+
+
+def init_state(n, r, D, Q, seed, stiefel=True, sigma_w=1.0):
+    """GPT_SGLD.jl:357-369 on the framework streams: w = σ_w·randn(Q); U_k polar factor of
+    Z = randn(r, n) (Stiefel) or randn(n,r)/sqrt(n) (non-Stiefel)."""
+    w = sigma_w * px.normals(Q, seed, 0, px.W_INIT, 0)
+    U = np.empty((n, r, D), order="F")
+    for k in range(D):
+        z = px.normals(r * n, seed, 0, px.U_INIT, k)
+        if stiefel:
+            U[:, :, k] = stiefel_init(z.reshape((r, n), order="F"))
+        else:
+            U[:, :, k] = z.reshape((r, n), order="F").T / math.sqrt(n)
+    return w, U
+
+
+# --------------------------------------------------------------------------- sampler
+def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed,
+                  langevin=True, stiefel=True, sigma_w=1.0, store_every=1,
+                  w_init=None, U_init=None, max_steps=None, record=False):
+    """GPT_SGLD.jl:345-448 (Generation D).  Returns (w_store, U_store, info).
+
+    ``store_every`` = 1 is the reference (a sample after every post-burn-in step);
+    ``store_every`` = numbatches keeps the epoch-end samples the scripts consume
+    (kin40kExperiment.jl:79).  ``max_steps`` truncates the run (for parity tests).
+    ``info`` holds the status (0 ok, 1 NaN in geodesic) and, with ``record``,
+    per-step gradient norms and fhat.
+    """
+    phi = np.asarray(phi, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64).ravel()
+    n, D, N = phi.shape
+    numbatches = -(-N // m)
+    if w_init is None or U_init is None:
+        w0, U0 = init_state(n, r, D, Q, param_seed, stiefel, sigma_w)
+    w = np.array(w0 if w_init is None else w_init, dtype=np.float64)
+    U = np.array(U0 if U_init is None else U_init, dtype=np.float64, order="F")
+    nstore = (maxepoch * numbatches) // store_every
+    w_store = np.zeros((Q, nstore), order="F")
+    U_store = np.zeros((n, r, D, nstore), order="F")
+    info = dict(status=0, gradw_norm=[], gradU_norm=[], fhat=[])
+    order = np.arange(N)
+    step = 0
+    for epoch in range(1, burnin + maxepoch + 1):
+        perm = px.randperm(N, param_seed, epoch - 1)
+        order = order[perm]                      # phi=phi[:,:,perm]; y=y[perm] (cumulative)
+        for batch in range(1, numbatches + 1):
+            if max_steps is not None and step >= max_steps:
+                return w_store, U_store, info
+            idx = order[m * (batch - 1): min(m * batch, N)]
+            phi_b = phi[:, :, idx]
+            y_b = y[idx]
+            g = gradients(phi_b, y_b, w, U, I, N, signal_var, sigma_w)
+            if record:
+                info["gradw_norm"].append(np.linalg.norm(g["gradw"]))
+                info["gradU_norm"].append([np.linalg.norm(g["gradU"][:, :, k]) for k in range(D)])
+                info["fhat"].append(g["fhat"].copy())
+            if langevin:
+                w = w + epsw * g["gradw"] / 2 + math.sqrt(epsw) * px.normals(Q, param_seed, step, px.W_NOISE, 0)
+            else:
+                w = w + epsw * g["gradw"] / 2
+            if stiefel:
+                for k in range(D):
+                    xi = px.normals(n * r, param_seed, step, px.U_NOISE, k).reshape((n, r), order="F")
+                    drive = math.sqrt(epsU) * g["gradU"][:, :, k] / 2
+                    mom = proj(U[:, :, k], drive + xi if langevin else drive)
+                    Un, ok = geod(U[:, :, k], mom, math.sqrt(epsU))
+                    if not ok:
+                        info["status"] = 1
+                        return np.zeros_like(w_store), np.zeros_like(U_store), info
+                    U[:, :, k] = Un
+            else:
+                upd = epsU * (g["gradU"] - n * U) / 2
+                if langevin:
+                    xi = np.stack([px.normals(n * r, param_seed, step, px.U_NOISE, k).reshape((n, r), order="F")
+                                   for k in range(D)], axis=2)
+                    upd = upd + math.sqrt(epsU) * xi
+                U = U + upd
+            if epoch > burnin:
+                s = (epoch - burnin - 1) * numbatches + (batch - 1)
+                if (s + 1) % store_every == 0:
+                    slot = (s + 1) // store_every - 1
+                    w_store[:, slot] = w
+                    U_store[:, :, :, slot] = U
+            step += 1
+    return w_store, U_store, info
+
+
+def GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0, **kw):
+    """GPT_SGLD_p.jl:146-243 (Generations A/B): ``sigma`` is the noise s.d. and
+    σ_w = sqrt(n^D/Q) (:155).  Follows GPTregression's batch labels (the ``y[batch]`` slip
+    at :222 is not reproduced)."""
+    n, D, _ = np.asarray(phi).shape
+    return GPTregression(phi, y, sigma ** 2, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed,
+                         sigma_w=math.sqrt(float(n) ** D / Q), **kw)
+
+
+def GPNT_SGLD(phi, y, signal_var, sigma_theta, m, eps_theta, decay_rate, burnin, maxepoch, param_seed):
+    """GPT_SGLD.jl:809-847 — full-theta RFF SGLD (config 1).  Returns theta_store (n, T)
+    or zeros(n) on NaN (:840-843)."""
+    phi = np.asarray(phi, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64).ravel()
+    n, N = phi.shape
+    numbatches = -(-N // m)
+    theta = sigma_theta * px.normals(n, param_seed, 0, px.THETA_INIT, 0)
+    store = np.empty((n, (maxepoch + burnin) * numbatches), order="F")
+    order = np.arange(N)
+    t = 0
+    for epoch in range(1, maxepoch + burnin + 1):
+        order = order[px.randperm(N, param_seed, epoch - 1)]
+        for batch in range(1, numbatches + 1):
+            t += 1
+            idx = order[m * (batch - 1): min(m * batch, N)]
+            pb = phi[:, idx]
+            yb = y[idx]
+            B = len(idx)
+            eps = eps_theta * t ** (-decay_rate)
+            grad = -theta / sigma_theta ** 2 + (N / B) * (pb @ (yb - pb.T @ theta)) / signal_var
+            theta = theta + eps * grad / 2 + math.sqrt(eps) * px.normals(n, param_seed, t - 1, px.THETA_NOISE, 0)
+            store[:, t - 1] = theta
+            if np.isnan(theta).any():
+                return np.zeros(n)
+    return store
+
+
+# --------------------------------------------------------------------------- evaluation
+def rmse(ytest, fhat, scale=1.0):
+    """kin40kExperiment.jl:83 — ytrainStd·‖ytest − pred‖/sqrt(Ntest)."""
+    ytest = np.asarray(ytest, dtype=np.float64).ravel()
+    return scale * np.linalg.norm(ytest - fhat) / math.sqrt(len(ytest))
+
+
+def posterior_mean_pred(w_store, U_store, I, phitest, cols=None):
+    """GPT_SGLD_p.jl:124-132 (``RMSE``): mean of pred over stored samples (all, or ``cols``)."""
+    cols = range(w_store.shape[1]) if cols is None else cols
+    acc = None
+    cnt = 0
+    for s in cols:
+        p = pred(w_store[:, s], U_store[:, :, :, s], I, phitest)
+        acc = p if acc is None else acc + p
+        cnt += 1
+    return acc / cnt

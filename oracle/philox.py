@@ -1,0 +1,99 @@
+"""Philox4x32-10 random streams — the RNG contract shared by the HIP path and the oracle.
+
+TEST INFRASTRUCTURE.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import anything under ``oracle/``; the product path
+(``gpt_amd``) never does.
+
+Julia's MersenneTwister/Ziggurat stream (``srand``/``randn``/``randperm``,
+GPT_SGLD.jl:357,360,365,373,412,420) cannot be reproduced here (no Julia), so the
+framework defines its own counter-based streams.  The *consumption points* follow the
+reference one for one (SURVEY.md §8(a) "RNG consumption order"):
+
+    stream        counter (c0, c1, c2, c3)           reference draw
+    ------------  ---------------------------------  -------------------------------
+    W_INIT        (e>>1, 0,      W_INIT,  0)           w = randn(Q)          :360
+    U_INIT        (e>>1, 0,      U_INIT,  k)           Z = randn(r, n)       :365
+    PERM          (i,    epoch,  PERM,    0)           randperm(N)           :373
+    W_NOISE       (e>>1, step,   W_NOISE, 0)           randn(Q)              :412
+    U_NOISE       (e>>1, step,   U_NOISE, k)           randn(n, r)           :420
+    THETA_INIT    (e>>1, 0,      TH_INIT, 0)           theta = randn(n)      :815
+    THETA_NOISE   (e>>1, t,      TH_NOISE,0)           randn(n)              :836
+
+key = (seed & 0xffffffff, seed >> 32).  Element ``e`` of a normal stream comes from the
+Philox block at c0 = e>>1: two 53-bit uniforms u1, u2 and the Box–Muller pair
+(z0, z1) = sqrt(-2 ln u1)·(cos 2πu2, sin 2πu2); element e takes z0 if e is even, z1 if
+odd.  Column-major element order matches Julia's ``randn(r, n)`` / ``randn(n, r)``.
+``randperm`` is Fisher–Yates from the top: for i = N-1 … 1, j = floor(u32(i)·(i+1)/2^32),
+swap(p[i], p[j]).
+"""
+import numpy as np
+
+M0 = np.uint64(0xD2511F53)
+M1 = np.uint64(0xCD9E8D57)
+W0 = np.uint32(0x9E3779B9)
+W1 = np.uint32(0xBB67AE85)
+MASK32 = np.uint64(0xFFFFFFFF)
+
+W_INIT, U_INIT, PERM, W_NOISE, U_NOISE, THETA_INIT, THETA_NOISE = 1, 2, 3, 4, 5, 6, 7
+
+
+def philox4x32(c0, c1, c2, c3, seed):
+    """Vectorised Philox4x32-10.  c* are uint32 arrays (broadcastable); returns 4 uint32 arrays."""
+    c0 = np.asarray(c0, dtype=np.uint32)
+    c1 = np.asarray(c1, dtype=np.uint32)
+    c2 = np.asarray(c2, dtype=np.uint32)
+    c3 = np.asarray(c3, dtype=np.uint32)
+    c0, c1, c2, c3 = np.broadcast_arrays(c0, c1, c2, c3)
+    c0 = c0.copy(); c1 = c1.copy(); c2 = c2.copy(); c3 = c3.copy()
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    k0 = np.uint32(seed & 0xFFFFFFFF)
+    k1 = np.uint32(seed >> 32)
+    with np.errstate(over="ignore"):
+        for rnd in range(10):
+            if rnd > 0:
+                k0 = np.uint32((int(k0) + int(W0)) & 0xFFFFFFFF)
+                k1 = np.uint32((int(k1) + int(W1)) & 0xFFFFFFFF)
+            p0 = M0 * c0.astype(np.uint64)
+            p1 = M1 * c2.astype(np.uint64)
+            hi0 = (p0 >> np.uint64(32)).astype(np.uint32)
+            lo0 = (p0 & MASK32).astype(np.uint32)
+            hi1 = (p1 >> np.uint64(32)).astype(np.uint32)
+            lo1 = (p1 & MASK32).astype(np.uint32)
+            c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+    return c0, c1, c2, c3
+
+
+def _u53(a, b):
+    """Two uint32 words -> uniform double in (0, 1) with 53 random bits."""
+    return ((a >> np.uint32(5)).astype(np.float64) * 67108864.0
+            + (b >> np.uint32(6)).astype(np.float64) + 0.5) * (1.0 / 9007199254740992.0)
+
+
+def normals(count, seed, c1, c2, c3):
+    """``count`` standard normals of stream (c1, c2, c3) — element e at index e."""
+    count = int(count)
+    nblk = (count + 1) // 2
+    x0, x1, x2, x3 = philox4x32(np.arange(nblk, dtype=np.uint32), c1, c2, c3, seed)
+    u1 = _u53(x0, x1)
+    u2 = _u53(x2, x3)
+    rad = np.sqrt(-2.0 * np.log(u1))
+    th = 2.0 * np.pi * u2
+    z = np.empty(2 * nblk, dtype=np.float64)
+    z[0::2] = rad * np.cos(th)
+    z[1::2] = rad * np.sin(th)
+    return z[:count]
+
+
+def randperm(N, seed, epoch):
+    """0-based permutation of range(N) (Fisher–Yates, PERM stream of ``epoch``)."""
+    N = int(N)
+    p = np.arange(N, dtype=np.int64)
+    if N <= 1:
+        return p
+    i = np.arange(N, dtype=np.uint32)
+    x0, _, _, _ = philox4x32(i, epoch, PERM, 0, seed)
+    x0 = x0.astype(np.uint64)
+    for ii in range(N - 1, 0, -1):
+        j = int((int(x0[ii]) * (ii + 1)) >> 32)
+        p[ii], p[j] = p[j], p[ii]
+    return p

@@ -1,0 +1,205 @@
+"""GPU parity: libgptsgld.so (HIP, gfx950) against the CPU oracle on identical inputs, seeds,
+Philox streams and permutations.
+
+Tolerances (fp64 path; the GPU sums in a different order and uses leave-one-out products
+instead of computeU_phi's division, GPT_SGLD.jl:253):
+  features                       max |Δ| <= 4e-16·|c|  (cos differs by ≤ 1 ulp between libms)
+  pred / fhat                    max |Δ| <= 1e-12·max|f|
+  sampler trajectories           max |Δ| <= 1e-8·max|x| over every stored w and U sample
+  per-step gradient norms        relative <= 1e-9
+  test RMSE                      relative <= 1e-10
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import gpt_sgld_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def G():
+    from gpt_amd import GPT_SGLD
+    return GPT_SGLD
+
+
+def rel(a, b):
+    a = np.asarray(a); b = np.asarray(b)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+
+
+def make_problem(n, D, N, r, Q, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((N, D))
+    Z = rng.standard_normal((n, D))
+    b = 2 * np.pi * rng.random((n, D))
+    ls = 1.0 + 0.2 * rng.standard_normal(D)
+    scale = math.sqrt(n / Q ** (1.0 / D))
+    phi = R.feature(X, ls, 1.0, scale, Z, b)
+    I = R.samplenz(r, D, Q, seed + 1)
+    w, U = R.init_state(n, r, D, Q, seed + 2)
+    y = R.pred(w, U, I, phi) + 0.05 * rng.standard_normal(N)
+    return dict(X=X, Z=Z, b=b, ls=ls, scale=scale, phi=phi, I=I, y=y)
+
+
+# ----------------------------------------------------------------------------- features
+def test_feature_matches_oracle():
+    rng = np.random.default_rng(1)
+    N, D, n = 300, 5, 64
+    X = rng.standard_normal((N, D)); Z = rng.standard_normal((n, D)); b = 2 * np.pi * rng.random((n, D))
+    ls = 1 + 0.2 * rng.standard_normal(D)
+    got = G().feature(X, ls, 1.3, 2.0, Z, b)
+    want = R.feature(X, ls, 1.3, 2.0, Z, b)
+    assert got.shape == (n, D, N)
+    assert np.abs(got - want).max() <= 4e-16 * np.abs(want).max() * 4
+
+
+def test_feature_seeded_generation_c():
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((50, 4))
+    got = G().feature(X, 20, [1.2, 1.1, 0.9, 1.4], 1.05, 17, 3.0)
+    Z, b = R.seeded_feature_inputs(20, 4, 17)
+    want = R.feature(X, [1.2, 1.1, 0.9, 1.4], 1.05, 3.0, Z, b)
+    assert rel(got, want) < 2e-15
+
+
+def test_feature_notensor_matches_oracle():
+    rng = np.random.default_rng(3)
+    N, D, n = 200, 4, 96
+    X = rng.standard_normal((N, D)); Z = rng.standard_normal((n, D)); b = 2 * np.pi * rng.random(n)
+    got = G().featureNotensor(X, 1.4332, 1.0, Z, b)
+    want = R.featureNotensor(X, 1.4332, 1.0, Z, b)
+    assert rel(got, want) < 2e-15
+
+
+# ----------------------------------------------------------------------------- prediction
+@pytest.mark.parametrize("tag,expected", [("5D", 0.03125), ("10D", 0.0258)])
+def test_pred_on_reference_fixture(tag, expected):
+    from conftest import load_golden
+    d = load_golden("tensor_synth_%s.npz" % tag)
+    f = G().pred(d["w"], d["U"], d["I"], d["phi"])
+    want = R.pred(d["w"], d["U"], d["I"], d["phi"])
+    assert rel(f, want) < 1e-12
+    assert abs(np.std(d["y3"] - f) - expected) < 5e-4
+
+
+def test_pred_mean_and_rmse():
+    p = make_problem(40, 4, 300, 3, 20, seed=5)
+    rng = np.random.default_rng(9)
+    S = 4
+    ws = rng.standard_normal((20, S))
+    Us = np.stack([R.init_state(40, 3, 4, 20, 100 + s)[1] for s in range(S)], axis=3)
+    mean, rm = G().pred_mean(ws, Us, p["I"], p["phi"], p["y"], scale=2.5)
+    want = R.posterior_mean_pred(ws, Us, p["I"], p["phi"])
+    assert rel(mean, want) < 1e-12
+    assert rm == pytest.approx(R.rmse(p["y"], want, 2.5), rel=1e-10)
+
+
+# ----------------------------------------------------------------------------- sampler
+CASES = {
+    # name: (n, D, N, r, Q, m, burnin, maxepoch, store_every, langevin, stiefel)
+    "small": (16, 3, 40, 2, 6, 8, 1, 2, 1, True, True),
+    "ragged_thin": (24, 4, 37, 3, 10, 8, 0, 3, 5, True, True),
+    "sgd": (16, 3, 40, 2, 6, 8, 0, 2, 1, False, True),
+    "euclid": (16, 3, 40, 2, 6, 8, 0, 2, 1, True, False),
+    "kin40k_shape": (500, 8, 200, 5, 200, 50, 0, 1, 1, True, True),
+    "wide_batch": (64, 4, 300, 4, 30, 100, 0, 1, 1, True, True),
+    "rank10": (100, 4, 120, 10, 60, 30, 0, 1, 1, True, True),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_sampler_trajectory_matches_oracle(name):
+    n, D, N, r, Q, m, burnin, maxepoch, se, lang, stf = CASES[name]
+    p = make_problem(n, D, N, r, Q, seed=11)
+    kw = dict(langevin=lang, stiefel=stf, store_every=se)
+    epsw, epsU, sv, seed = 1e-4, 1e-6, 0.05, 23
+    ws, Us, dg = G().GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
+                                   maxepoch, seed, diag=True, **kw)
+    wo, Uo, info = R.GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
+                                   maxepoch, seed, record=True, **kw)
+    assert info["status"] == 0
+    assert ws.shape == wo.shape and Us.shape == Uo.shape
+    assert rel(ws, wo) < 1e-8, rel(ws, wo)
+    assert rel(Us, Uo) < 1e-8, rel(Us, Uo)
+    gw = np.array(info["gradw_norm"]); gU = np.array(info["gradU_norm"]).T
+    assert rel(dg[0], gw) < 1e-9
+    assert rel(dg[1:], gU) < 1e-9
+    if stf:
+        for s in range(Us.shape[3]):
+            for k in range(D):
+                Uk = Us[:, :, k, s]
+                assert np.abs(Uk.T @ Uk - np.eye(r)).max() < 1e-10
+
+
+def test_sgldERM_generation_a_mapping():
+    n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
+    p = make_problem(n, D, N, r, Q, seed=4)
+    ws, Us = G().GPT_SGLDERM(p["phi"], p["y"], 0.3, p["I"], r, Q, m, 1e-6, 1e-6, 0, 2, 3)
+    wo, Uo, _ = R.GPT_SGLDERM(p["phi"], p["y"], 0.3, p["I"], r, Q, m, 1e-6, 1e-6, 0, 2, 3)
+    assert rel(ws, wo) < 1e-8 and rel(Us, Uo) < 1e-8
+
+
+def test_injected_initial_state():
+    n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
+    p = make_problem(n, D, N, r, Q, seed=8)
+    rng = np.random.default_rng(0)
+    w0 = rng.standard_normal(Q)
+    _, U0 = R.init_state(n, r, D, Q, 999)
+    ws, Us = G().GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e-6, 0, 1, 4,
+                               w_init=w0, U_init=U0)
+    wo, Uo, _ = R.GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e-6, 0, 1, 4,
+                                w_init=w0, U_init=U0)
+    assert rel(ws, wo) < 1e-8 and rel(Us, Uo) < 1e-8
+
+
+def test_nan_geodesic_bailout_zero_fills(capsys):
+    n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
+    p = make_problem(n, D, N, r, Q, seed=6)
+    ws, Us = G().GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e300, 0, 2, 3)
+    assert not ws.any() and not Us.any()
+    assert "Get NaN when moving along Geodesic" in capsys.readouterr().out
+    _, _, info = R.GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e300, 0, 2, 3)
+    assert info["status"] == 1
+
+
+def test_bad_dims_raise():
+    from gpt_amd._lib import GPTError
+    p = make_problem(8, 3, 20, 2, 5, seed=1)
+    with pytest.raises((GPTError, ValueError)):
+        G().GPTregression(p["phi"], p["y"], 0.1, p["I"], 7, 5, 4, 1e-4, 1e-6, 0, 1, 1)  # r=7
+    with pytest.raises((GPTError, ValueError)):
+        G().GPTregression(p["phi"], p["y"], 0.1, p["I"], 2, 5000, 4, 1e-4, 1e-6, 0, 1, 1)
+
+
+def test_gpnt_sgld_matches_oracle():
+    rng = np.random.default_rng(12)
+    N, D, n = 120, 4, 80
+    X = rng.standard_normal((N, D)); Z = rng.standard_normal((n, D)); b = 2 * np.pi * rng.random(n)
+    phi = R.featureNotensor(X, 1.4, 1.0, Z, b)
+    y = rng.standard_normal(N)
+    got = G().GPNT_SGLD(phi, y, 0.05, 1.0, 25, 1e-4, 0.1, 1, 2, 5)
+    want = R.GPNT_SGLD(phi, y, 0.05, 1.0, 25, 1e-4, 0.1, 1, 2, 5)
+    assert got.shape == want.shape
+    assert rel(got, want) < 1e-9
+
+
+def test_multichain_session_equals_single_runs():
+    import torch
+    from gpt_amd.session import SGLDSession
+    n, D, N, r, Q, m = 32, 4, 60, 3, 12, 16
+    p = make_problem(n, D, N, r, Q, seed=21)
+    phi_t = torch.from_numpy(np.ascontiguousarray(p["phi"].transpose(2, 1, 0))).cuda()
+    y_t = torch.from_numpy(p["y"]).cuda()
+    seeds = [3, 4, 5]
+    s = SGLDSession(phi_t, y_t, p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 2, seeds, store_every=2)
+    s.run(3)          # partial chunk, then the rest through the captured graph
+    s.run(10 ** 9)
+    s.sync()
+    for c, sd in enumerate(seeds):
+        ws, Us, st = s.fetch(c)
+        wo, Uo, _ = R.GPTregression(p["phi"], p["y"], 0.05, p["I"], r, Q, m, 1e-4, 1e-6, 0, 2, sd,
+                                    store_every=2)
+        assert st == 0 and rel(ws, wo) < 1e-8 and rel(Us, Uo) < 1e-8
+    s.close()
