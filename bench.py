@@ -90,8 +90,11 @@ def main():
     ap.add_argument("--r", type=int, default=5)
     ap.add_argument("--Q", type=int, default=200)
     ap.add_argument("--m", type=int, default=50)
-    ap.add_argument("--epsw", type=float, default=1e-4)
-    ap.add_argument("--epsU", type=float, default=1e-7)
+    # kin40kExperiment.jl:50-51 uses εw=1e-4, εU=1e-7 at n=150, r=20; under the restated
+    # GPT_SGLD.jl update both the oracle and the GPU path diverge there (w Hessian λmax≈3e5),
+    # so the benchmark uses the largest stable pair found by the oracle sweep.
+    ap.add_argument("--epsw", type=float, default=1e-5)
+    ap.add_argument("--epsU", type=float, default=1e-8)
     ap.add_argument("--signal_var", type=float, default=0.0476)
     ap.add_argument("--kernel-steps", type=int, default=100, help="steps of the event-timed pass")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -156,6 +159,10 @@ def main():
 
     # per-launch kernel time (hipEvents around each step-kernel launch on the session stream)
     k_us = sess.time_steps(args.kernel_steps)
+    sess.sync()
+    bad = [c for c in range(C) if sess.fetch(c)[2] != 0]
+    if bad:
+        raise SystemExit("chains %s hit the geodesic NaN bail-out: the timed steps were no-ops" % bad)
     B = m
     bytes_launch = C * algorithmic_bytes_per_step(n, D, B, r, Q)
     achieved = bytes_launch / (k_us * 1e-6) / 1e9

@@ -44,12 +44,15 @@ SIGNATURES = {
                                           C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), P_I32,
                                           C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]),
     "gpt_sgld_session_run": (C.c_int, [C.c_void_p, C.c_int64]),
+    "gpt_sgld_session_set_hyper": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_double,
+                                             C.c_double, C.c_double]),
     "gpt_sgld_session_sync": (C.c_int, [C.c_void_p]),
     "gpt_sgld_session_state": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p),
                                          C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                          C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
     "gpt_sgld_session_steps_done": (C.c_int64, [C.c_void_p]),
     "gpt_sgld_session_time_steps": (C.c_int, [C.c_void_p, C.c_int64, P_D]),
+    "gpt_sgld_session_stamps": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
     "gpt_feature_dev": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
                                   C.c_double, C.c_double, C.c_void_p, C.c_void_p, C.c_int64,
                                   C.c_void_p, C.c_void_p]),
@@ -65,11 +68,19 @@ SIGNATURES = {
     "gpt_gpnt_sgld": (C.c_int, [P_D, P_D, C.c_int64, C.c_int64, C.c_double, C.c_double, C.c_int64,
                                 C.c_double, C.c_double, C.c_int64, C.c_int64, C.c_uint64, P_D]),
     "gpt_last_error": (C.c_char_p, []),
+    "gpt_sgld_lds_bytes": (C.c_int64, [C.c_int64] * 5),
     "gpt_device_count": (C.c_int, []),
 }
 
 
 def load(path=LIB_PATH):
+    # Bind to the HIP runtime torch already carries (one runtime per process): torch's
+    # bundled libamdhip64 has the same soname, so loading torch first makes the dynamic
+    # loader resolve our NEEDED entry to it instead of pulling in a second runtime.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(path):
         raise ImportError(
             "libgptsgld.so not found at %s — build it with `python -c \"import __graft_entry__ as g; "

@@ -195,6 +195,10 @@ struct gpt_sgld_session {
 
 extern "C" const char* gpt_last_error(void) { return g_err.c_str(); }
 
+extern "C" int64_t gpt_sgld_lds_bytes(int64_t n, int64_t D, int64_t r, int64_t Q, int64_t m) {
+  return (int64_t)step_layout((int)n, (int)D, (int)r, (int)Q, (int)m).bytes;
+}
+
 extern "C" int gpt_device_count(void) {
   int c = 0;
   if (hipGetDeviceCount(&c) != hipSuccess) return 0;
@@ -251,13 +255,13 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   P.total_steps = s->total_steps;
   P.store_every = (int)cfg->store_every;
   P.langevin = cfg->langevin; P.stiefel = cfg->stiefel;
-  P.signal_var = cfg->signal_var; P.sigma_w = cfg->sigma_w; P.epsw = cfg->epsw; P.epsU = cfg->epsU;
 
   std::vector<int32_t> I0((size_t)Q * D);
   for (size_t x = 0; x < I0.size(); ++x) I0[x] = I_host[x] - 1;
   HIPCHK(s->I0.alloc(sizeof(int32_t) * I0.size()));
   HIPCHK(hipMemcpy(s->I0.p, I0.data(), sizeof(int32_t) * I0.size(), hipMemcpyHostToDevice));
   P.I0 = s->I0.as<int32_t>();
+  P.stamps = nullptr;
   HIPCHK(s->tbase.alloc(sizeof(long long)));
   HIPCHK(hipMemset(s->tbase.p, 0, sizeof(long long)));
   HIPCHK(s->status.alloc(sizeof(int32_t) * nchains));
@@ -290,6 +294,7 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     C.diag = s->diag ? (double*)(base + b_w + b_U + b_temp + b_ord + b_ws + b_Us) : nullptr;
     C.status = s->status.as<int32_t>() + c;
     C.seed = seeds[c];
+    C.epsw = cfg->epsw; C.epsU = cfg->epsU; C.signal_var = cfg->signal_var; C.sigma_w = cfg->sigma_w;
     host_init_state(n, r, D, Q, seeds[c], cfg->stiefel != 0, cfg->sigma_w, w0.data(), U0.data());
     host_epoch_orders(N, seeds[c], s->epochs, ord.data());
     HIPCHK(hipMemcpy(C.w, w0.data(), 8 * (size_t)Q, hipMemcpyHostToDevice));
@@ -313,6 +318,16 @@ static int session_set_state(gpt_sgld_session* s, int c, const double* w, const 
   if (w) HIPCHK(hipMemcpy(C.w, w, 8 * (size_t)s->P.Q, hipMemcpyHostToDevice));
   if (U) HIPCHK(hipMemcpy(C.U, U, 8 * (size_t)s->P.n * s->P.r * s->P.D, hipMemcpyHostToDevice));
   s->temp_ready = false;
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_set_hyper(gpt_sgld_session* s, int32_t chain, double epsw,
+                                          double epsU, double signal_var, double sigma_w) {
+  if (!s || chain < 0 || chain >= s->nchains) { set_error("bad chain"); return GPT_ERR_BAD_DIMS; }
+  if (!(signal_var > 0) || !(sigma_w > 0)) { set_error("variances must be > 0"); return GPT_ERR_BAD_DIMS; }
+  ChainDesc& C = s->chains_h[chain];
+  C.epsw = epsw; C.epsU = epsU; C.signal_var = signal_var; C.sigma_w = sigma_w;
+  HIPCHK(hipMemcpy(s->chains_d.as<ChainDesc>() + chain, &C, sizeof(ChainDesc), hipMemcpyHostToDevice));
   return GPT_OK;
 }
 
@@ -386,6 +401,35 @@ extern "C" int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, 
   if (rc != GPT_OK) return rc;
   s->steps_done += cnt;
   if (avg_us) *avg_us = 1000.0 * tot / (double)cnt;
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out) {
+  if (!s || !out) { set_error("null argument"); return GPT_ERR_BAD_DIMS; }
+  const long long cnt = std::min<long long>(nsteps, s->total_steps - s->steps_done);
+  if (cnt <= 0) return GPT_OK;
+  if (!s->temp_ready) {
+    hipError_t e = launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
+                                    s->tbase.as<long long>(), s->stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_temp_init");
+    s->temp_ready = true;
+  }
+  const size_t per = (size_t)(s->P.D + 1) * s->nchains * kStamps;
+  DevMem buf;
+  HIPCHK(buf.alloc(8 * per * cnt));
+  HIPCHK(hipMemset(buf.p, 0, 8 * per * cnt));
+  StepParams P = s->P;
+  for (long long i = 0; i < cnt; ++i) {
+    P.stamps = buf.as<long long>() + per * i;
+    hipError_t e = launch_step(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
+                               (int)i, s->stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_step");
+  }
+  hipError_t e = launch_advance(s->tbase.as<long long>(), cnt, s->stream);
+  if (e != hipSuccess) return hip_fail(e, "launch_advance");
+  HIPCHK(hipStreamSynchronize(s->stream));
+  HIPCHK(hipMemcpy(out, buf.p, 8 * per * cnt, hipMemcpyDeviceToHost));
+  s->steps_done += cnt;
   return GPT_OK;
 }
 

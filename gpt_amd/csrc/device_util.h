@@ -78,11 +78,11 @@ struct RCfg {
 // temp[l][i] = Σ_j phi[koff + row(i)*rstride + j] · U_l[l*NP + j]   (GPT_SGLD.jl:193-205)
 // for i < Bt, row(i) = idx_l[i].  Lanes stride over j (coalesced 512-B loads), wave w takes
 // columns i = base + w + kNW·ii; partials are combined with one Butterfly per pass.
-// U_l rows must be zero-padded for j in [n, NP).
+// U_l rows (stride NS) must be zero-padded for j in [n, NP).
 template <int R, class Out>
 __device__ __forceinline__ void phidotU_tile(const double* __restrict__ phi, long long koff,
                                              long long rstride, const int* idx_l, int Bt,
-                                             int n, int NP, const double* U_l, Out out) {
+                                             int n, int NP, int NS, const double* U_l, Out out) {
   using C = RCfg<R>;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   constexpr int SH = 6 - Butterfly<C::NV>::P;
@@ -90,14 +90,14 @@ __device__ __forceinline__ void phidotU_tile(const double* __restrict__ phi, lon
     double v[C::NV];
 #pragma unroll
     for (int u = 0; u < C::NV; ++u) v[u] = 0.0;
-    const double* rowp[C::ICH];
+    const __attribute__((address_space(1))) double* rowp[C::ICH];
 #pragma unroll
     for (int ii = 0; ii < C::ICH; ++ii) {
       const int i = min(base + wv + kNW * ii, Bt - 1);
-      rowp[ii] = phi + koff + (long long)uni(idx_l[i]) * rstride;
+      rowp[ii] = gptr(phi) + koff + (long long)uni(idx_l[i]) * rstride;
     }
     const int JS = NP >> 6;
-#pragma unroll 2
+#pragma unroll 4
     for (int s = 0; s < JS; ++s) {
       const int j = lane + 64 * s;
       const int jc = min(j, n - 1);
@@ -106,7 +106,7 @@ __device__ __forceinline__ void phidotU_tile(const double* __restrict__ phi, lon
       for (int ii = 0; ii < C::ICH; ++ii) p[ii] = rowp[ii][jc];
       double u[R];
 #pragma unroll
-      for (int l = 0; l < R; ++l) u[l] = U_l[l * NP + j];
+      for (int l = 0; l < R; ++l) u[l] = U_l[l * NS + j];
 #pragma unroll
       for (int ii = 0; ii < C::ICH; ++ii)
 #pragma unroll
@@ -122,46 +122,62 @@ __device__ __forceinline__ void phidotU_tile(const double* __restrict__ phi, lon
   }
 }
 
-// V-phase partials for columns [ic, ic+64) (lane = column): over q = wave, wave+kNW, …
-//   V[q,i]  = Π_k temp[k, I[q,k], i]                 (GPT_SGLD.jl:208-220, same k order)
-//   fh     += w[q]·V[q,i]                            (:223-230)
-//   a[l]   += w[q]·Π_{k'≠kown} temp[k', I[q,k'], i]  for l = I[q,kown]   (:246-273, no division)
-// writes red[(wave*(1+R) + comp)*64 + lane]; comp 0 = fh, 1+l = a[l].
-template <int R>
-__device__ __forceinline__ void vphase_partials(const double* temp_l, int MP, const int* I_l,
-                                                const double* w_l, int Q, int D, int kown,
-                                                int ic, int Bt, double* red) {
+// V-phase over a batch (lanes = core entries q, strided by 64; waves = batch columns
+// i = base + wave + kNW·ii).  For each column, with NC = 1 + R values per column:
+//   val[0]   = Σ_q w[q]·V[q,i],  V[q,i] = Π_k temp[k, I[q,k], i]      (GPT_SGLD.jl:208-230, k order)
+//   val[1+l] = Σ_{q: I[q,kown]=l} w[q]·Π_{k≠kown} temp[k, I[q,k], i]   (:246-273 without the
+//              division of computeU_phi — a leave-one-out product)
+// reduced over q by one Butterfly per pass (no cross-wave traffic).  IT_l is I transposed
+// (kk·Q + q, conflict-free per-lane reads).  out(comp, i, value) is called once per value.
+template <int R, class Out>
+__device__ __forceinline__ void vphase_tile(const double* temp_l, int MP, const int* IT_l,
+                                            const double* w_l, int Q, int D, int kown, int Bt,
+                                            Out out) {
+  constexpr int NC = 1 + R;
+  constexpr int ICV = (64 / NC) < 12 ? (64 / NC) : 12;   // columns per wave pass
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int i = min(ic + lane, Bt - 1);
-  double fh = 0.0;
-  double a[R];
+  for (int base = 0; base < Bt; base += kNW * ICV) {
+    const int nii = min(ICV, (Bt - base - wv + kNW - 1) / kNW);
+    int col[ICV];
 #pragma unroll
-  for (int l = 0; l < R; ++l) a[l] = 0.0;
-  for (int q = wv; q < Q; q += kNW) {
-    const int* Iq = I_l + q * D;
-    double v = 1.0, vk = 1.0;
+    for (int ii = 0; ii < ICV; ++ii) col[ii] = min(base + wv + kNW * ii, Bt - 1);
+    double v[64];
 #pragma unroll
-    for (int kk = 0; kk < kDMax; ++kk) {
-      if (kk < D) {
-        const double tv = temp_l[(kk * R + uni(Iq[kk])) * MP + i];
-        v *= tv;
-        if (kk != kown) vk *= tv;
+    for (int u = 0; u < 64; ++u) v[u] = 0.0;
+    for (int q0 = 0; q0 < Q; q0 += 64) {
+      const int q = q0 + lane;
+      const bool ok = q < Q;
+      const int qq = ok ? q : 0;
+      const double wq = ok ? w_l[qq] : 0.0;
+      const int lk = IT_l[kown * Q + qq];
+      double vv[ICV], vk[ICV];
+#pragma unroll
+      for (int ii = 0; ii < ICV; ++ii) { vv[ii] = 1.0; vk[ii] = 1.0; }
+      // k outer (same product order as computeV), the ICV column loads of one k in flight
+      for (int kk = 0; kk < D; ++kk) {
+        const double* row = temp_l + (kk * R + IT_l[kk * Q + qq]) * MP;
+        double tv[ICV];
+#pragma unroll
+        for (int ii = 0; ii < ICV; ++ii) tv[ii] = row[col[ii]];
+        if (kk != kown) {
+#pragma unroll
+          for (int ii = 0; ii < ICV; ++ii) { vv[ii] *= tv[ii]; vk[ii] *= tv[ii]; }
+        } else {
+#pragma unroll
+          for (int ii = 0; ii < ICV; ++ii) vv[ii] *= tv[ii];
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < ICV; ++ii) {
+        v[ii * NC] = fma(wq, vv[ii], v[ii * NC]);
+        const double cc = wq * vk[ii];
+#pragma unroll
+        for (int l = 0; l < R; ++l) v[ii * NC + 1 + l] += (l == lk) ? cc : 0.0;
       }
     }
-    const double wq = w_l[q];
-    fh = fma(wq, v, fh);
-    if (kown >= 0) {
-      const int lk = uni(Iq[kown]);
-      const double cc = wq * vk;
-#pragma unroll
-      for (int l = 0; l < R; ++l)
-        if (l == lk) a[l] += cc;
-    }
-  }
-  red[(wv * (1 + R)) * 64 + lane] = fh;
-  if (kown >= 0) {
-#pragma unroll
-    for (int l = 0; l < R; ++l) red[(wv * (1 + R) + 1 + l) * 64 + lane] = a[l];
+    Butterfly<64>::run(v, lane);
+    const int ii = lane / NC, comp = lane - ii * NC;
+    if (ii < nii) out(comp, base + wv + kNW * ii, v[0]);
   }
 }
 
@@ -186,9 +202,17 @@ __device__ __forceinline__ void blk_gram(const double* X, const double* Y, int N
       xa = (o < R * R ? X : Y) + a * NP;
       yb = Y + b * NP;
     }
-    double s = 0.0;
-    for (int j = j0; j < j1; ++j) s = fma(xa[j], yb[j], s);
-    red[wv * nout + o] = s;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int j = j0;
+    for (; j + 8 <= j1; j += 8) {
+      double x[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { x[u] = xa[j + u]; y[u] = yb[j + u]; }
+      s0 = fma(x[0], y[0], s0); s1 = fma(x[1], y[1], s1); s2 = fma(x[2], y[2], s2); s3 = fma(x[3], y[3], s3);
+      s0 = fma(x[4], y[4], s0); s1 = fma(x[5], y[5], s1); s2 = fma(x[6], y[6], s2); s3 = fma(x[7], y[7], s3);
+    }
+    for (; j < j1; ++j) s0 = fma(xa[j], yb[j], s0);
+    red[wv * nout + o] = (s0 + s1) + (s2 + s3);
   }
   __syncthreads();
   for (int o = threadIdx.x; o < nout; o += kNT) {
@@ -201,12 +225,26 @@ __device__ __forceinline__ void blk_gram(const double* X, const double* Y, int N
 }
 
 // ---------------------------------------------------------------- small dense algebra (1 wave)
-__device__ __forceinline__ void wave_mm(const double* A, const double* B, double* C, int nn) {
+// Padé numerator coefficients b_0..b_m of degrees 3, 5, 7, 9 (Higham 2005, Julia Base expm!).
+__constant__ double kPade[4][10] = {
+    {120.0, 60.0, 12.0, 1.0},
+    {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0},
+    {17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0},
+    {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0, 2162160.0, 110880.0,
+     3960.0, 90.0, 1.0}};
+
+// NN is compile-time so every inner product is unrolled with all its LDS reads in flight.
+template <int NN>
+__device__ __forceinline__ void wave_mm(const double* A, const double* B, double* C) {
   const int lane = threadIdx.x & 63;
-  for (int o = lane; o < nn * nn; o += 64) {
-    const int i = o / nn, j = o - i * nn;
+  for (int o = lane; o < NN * NN; o += 64) {
+    const int i = o / NN, j = o - i * NN;
+    double a[NN], b[NN];
+#pragma unroll
+    for (int t = 0; t < NN; ++t) { a[t] = A[i * NN + t]; b[t] = B[t * NN + j]; }
     double s = 0.0;
-    for (int t = 0; t < nn; ++t) s = fma(A[i * nn + t], B[t * nn + j], s);
+#pragma unroll
+    for (int t = 0; t < NN; ++t) s = fma(a[t], b[t], s);
     C[o] = s;
   }
   wave_sync();
@@ -214,60 +252,63 @@ __device__ __forceinline__ void wave_mm(const double* A, const double* B, double
 
 // Solve M·X = X0 in place (X holds X0 on entry), partial pivoting (LAPACK gesv semantics:
 // largest |pivot|, first index on ties, multipliers scaled by 1/pivot).
-__device__ __forceinline__ void wave_solve(double* M, double* X, int nn) {
+template <int NN>
+__device__ __forceinline__ void wave_solve(double* M, double* X) {
   const int lane = threadIdx.x & 63;
-  for (int c = 0; c < nn; ++c) {
-    double best = -1.0;
-    int bi = c;
-    if (lane >= c && lane < nn) { best = fabs(M[lane * nn + c]); bi = lane; }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double ob = __shfl_xor(best, off, 64);
-      const int oi = __shfl_xor(bi, off, 64);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-    }
-    bi = uni(bi);
+  for (int c = 0; c < NN; ++c) {
+    const double mine = (lane >= c && lane < NN) ? fabs(M[lane * NN + c]) : -1.0;
+    const double best = wave_max(mine);
+    const unsigned long long hit = __ballot(mine == best && lane >= c && lane < NN);
+    const int bi = hit ? (int)__ffsll((long long)hit) - 1 : c;
     if (bi != c) {
-      for (int col = lane; col < nn; col += 64) {
-        double t0 = M[c * nn + col]; M[c * nn + col] = M[bi * nn + col]; M[bi * nn + col] = t0;
-        double t1 = X[c * nn + col]; X[c * nn + col] = X[bi * nn + col]; X[bi * nn + col] = t1;
+      for (int col = lane; col < NN; col += 64) {
+        double t0 = M[c * NN + col]; M[c * NN + col] = M[bi * NN + col]; M[bi * NN + col] = t0;
+        double t1 = X[c * NN + col]; X[c * NN + col] = X[bi * NN + col]; X[bi * NN + col] = t1;
       }
       wave_sync();
     }
-    const double rp = 1.0 / M[c * nn + c];
-    const int rows = nn - c - 1;
-    // row updates: M[row][col>c] and X[row][*]
-    const int wcols = (nn - c - 1) + nn;
+    const double rp = 1.0 / M[c * NN + c];
+    const int rows = NN - c - 1;
+    const int wcols = (NN - c - 1) + NN;
     for (int o = lane; o < rows * wcols; o += 64) {
       const int rr = c + 1 + o / wcols, cc = o - (o / wcols) * wcols;
-      const double f = M[rr * nn + c] * rp;
-      if (cc < nn - c - 1) {
+      const double f = M[rr * NN + c] * rp;
+      if (cc < NN - c - 1) {
         const int col = c + 1 + cc;
-        M[rr * nn + col] -= f * M[c * nn + col];
+        M[rr * NN + col] -= f * M[c * NN + col];
       } else {
-        const int col = cc - (nn - c - 1);
-        X[rr * nn + col] -= f * X[c * nn + col];
+        const int col = cc - (NN - c - 1);
+        X[rr * NN + col] -= f * X[c * NN + col];
       }
     }
     wave_sync();
   }
-  for (int c = nn - 1; c >= 0; --c) {
-    for (int col = lane; col < nn; col += 64) {
-      double s = X[c * nn + col];
-      for (int t = c + 1; t < nn; ++t) s -= M[c * nn + t] * X[t * nn + col];
-      X[c * nn + col] = s / M[c * nn + c];
+  // back substitution: lanes over columns of X; the row of M and the solved rows stay in regs
+  for (int col = lane; col < NN; col += 64) {
+    double x[NN];
+#pragma unroll
+    for (int t = 0; t < NN; ++t) x[t] = X[t * NN + col];
+#pragma unroll
+    for (int c = NN - 1; c >= 0; --c) {
+      double s = x[c];
+#pragma unroll
+      for (int t = c + 1; t < NN; ++t) s -= M[c * NN + t] * x[t];
+      x[c] = s / M[c * NN + c];
     }
-    wave_sync();
+#pragma unroll
+    for (int t = 0; t < NN; ++t) X[t * NN + col] = x[t];
   }
+  wave_sync();
 }
 
-// X = expm(A) for an nn×nn matrix held in S[0..nn²) (row-major; overwritten).  Padé
+// expm(A) for an NN×NN matrix held in S[0..NN²) (row-major; overwritten).  Padé
 // scaling-and-squaring of Julia Base 0.3 expm! (Higham 2005; thresholds 0.015/0.25/0.95/2.1,
-// 13th order above, θ13 = 5.4).  Scratch S: 8 nn² doubles; result at S + 8 nn².
+// 13th order above, θ13 = 5.4).  Scratch S: 7 NN² doubles; the result is left at S + NN².
 // Returns true if the result contains a NaN (the geod bail-out of GPT_SGLD.jl:23-26).
-__device__ bool wave_expm(double* S, int nn) {
+template <int NN>
+__device__ bool wave_expm(double* S) {
   const int lane = threadIdx.x & 63;
-  const int q = nn * nn;
+  constexpr int q = NN * NN;
   double* A = S;
   double* A2 = S + q;
   double* A4 = S + 2 * q;
@@ -275,53 +316,37 @@ __device__ bool wave_expm(double* S, int nn) {
   double* U = S + 4 * q;
   double* V = S + 5 * q;
   double* T = S + 6 * q;
-  double* M = S + 7 * q;
-  double* X = S + 8 * q;
   double cs = 0.0;
-  if (lane < nn)
-    for (int i = 0; i < nn; ++i) cs += fabs(A[i * nn + lane]);
+  if (lane < NN) {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) cs += fabs(A[i * NN + lane]);
+  }
   const double nA = wave_max(cs);
   int si = 0;
   if (nA <= 2.1) {
-    double C[10];
-    int deg;
-    if (nA > 0.95) {
-      const double c9[10] = {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0,
-                             2162160.0, 110880.0, 3960.0, 90.0, 1.0};
-      for (int z = 0; z < 10; ++z) C[z] = c9[z];
-      deg = 9;
-    } else if (nA > 0.25) {
-      const double c7[8] = {17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0};
-      for (int z = 0; z < 8; ++z) C[z] = c7[z];
-      deg = 7;
-    } else if (nA > 0.015) {
-      const double c5[6] = {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0};
-      for (int z = 0; z < 6; ++z) C[z] = c5[z];
-      deg = 5;
-    } else {
-      const double c3[4] = {120.0, 60.0, 12.0, 1.0};
-      for (int z = 0; z < 4; ++z) C[z] = c3[z];
-      deg = 3;
-    }
-    wave_mm(A, A, A2, nn);
+    const int deg = nA > 0.95 ? 9 : (nA > 0.25 ? 7 : (nA > 0.015 ? 5 : 3));
+    const double* C = kPade[(deg - 3) / 2];   // wave-uniform: scalar loads from constant memory
+    wave_mm<NN>(A, A, A2);
+    const double c0 = C[0], c1 = C[1];
     for (int o = lane; o < q; o += 64) {
-      const double id = (o / nn == o - (o / nn) * nn) ? 1.0 : 0.0;
+      const double id = (o / NN == o - (o / NN) * NN) ? 1.0 : 0.0;
       T[o] = id;
-      U[o] = C[1] * id;
-      V[o] = C[0] * id;
+      U[o] = c1 * id;
+      V[o] = c0 * id;
     }
     wave_sync();
     for (int kk = 1; kk <= (deg - 1) / 2; ++kk) {
-      wave_mm(T, A2, A4, nn);  // P = P·A2  (A4 is free scratch here)
+      wave_mm<NN>(T, A2, A4);  // P = P·A2  (A4 is free scratch here)
+      const double cu = C[2 * kk + 1], cv = C[2 * kk];
       for (int o = lane; o < q; o += 64) {
         const double p = A4[o];
         T[o] = p;
-        U[o] = U[o] + C[2 * kk + 1] * p;
-        V[o] = V[o] + C[2 * kk] * p;
+        U[o] = U[o] + cu * p;
+        V[o] = V[o] + cv * p;
       }
       wave_sync();
     }
-    wave_mm(A, U, A6, nn);
+    wave_mm<NN>(A, U, A6);
     for (int o = lane; o < q; o += 64) U[o] = A6[o];
     wave_sync();
   } else {
@@ -333,38 +358,40 @@ __device__ bool wave_expm(double* S, int nn) {
       for (int o = lane; o < q; o += 64) A[o] *= sc;
       wave_sync();
     }
-    const double c[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
-                          1187353796428800.0, 129060195264000.0, 10559470521600.0,
-                          670442572800.0, 33522128640.0, 1323241920.0, 40840800.0, 960960.0,
-                          16380.0, 182.0, 1.0};
-    wave_mm(A, A, A2, nn);
-    wave_mm(A2, A2, A4, nn);
-    wave_mm(A2, A4, A6, nn);
+    constexpr double c[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
+                              1187353796428800.0, 129060195264000.0, 10559470521600.0,
+                              670442572800.0, 33522128640.0, 1323241920.0, 40840800.0, 960960.0,
+                              16380.0, 182.0, 1.0};
+    wave_mm<NN>(A, A, A2);
+    wave_mm<NN>(A2, A2, A4);
+    wave_mm<NN>(A2, A4, A6);
     for (int o = lane; o < q; o += 64) T[o] = c[13] * A6[o] + c[11] * A4[o] + c[9] * A2[o];
     wave_sync();
-    wave_mm(A6, T, M, nn);
+    wave_mm<NN>(A6, T, V);               // V used as scratch for A6·inner
     for (int o = lane; o < q; o += 64) {
-      const double id = (o / nn == o - (o / nn) * nn) ? 1.0 : 0.0;
-      M[o] = M[o] + c[7] * A6[o] + c[5] * A4[o] + c[3] * A2[o] + c[1] * id;
+      const double id = (o / NN == o - (o / NN) * NN) ? 1.0 : 0.0;
+      V[o] = V[o] + c[7] * A6[o] + c[5] * A4[o] + c[3] * A2[o] + c[1] * id;
       T[o] = c[12] * A6[o] + c[10] * A4[o] + c[8] * A2[o];
     }
     wave_sync();
-    wave_mm(A, M, U, nn);
-    wave_mm(A6, T, V, nn);
+    wave_mm<NN>(A, V, U);                // U = A·(A6·inner + …)
+    wave_mm<NN>(A6, T, V);               // V = A6·(…)
     for (int o = lane; o < q; o += 64) {
-      const double id = (o / nn == o - (o / nn) * nn) ? 1.0 : 0.0;
+      const double id = (o / NN == o - (o / NN) * NN) ? 1.0 : 0.0;
       V[o] = V[o] + c[6] * A6[o] + c[4] * A4[o] + c[2] * A2[o] + c[0] * id;
     }
     wave_sync();
   }
+  double* M = A4;      // dead from here on
+  double* X = A2;
   for (int o = lane; o < q; o += 64) {
     M[o] = V[o] - U[o];
     X[o] = V[o] + U[o];
   }
   wave_sync();
-  wave_solve(M, X, nn);
+  wave_solve<NN>(M, X);
   for (int z = 0; z < si; ++z) {
-    wave_mm(X, X, T, nn);
+    wave_mm<NN>(X, X, T);
     for (int o = lane; o < q; o += 64) X[o] = T[o];
     wave_sync();
   }

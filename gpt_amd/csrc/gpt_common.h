@@ -46,4 +46,27 @@ GPT_HD double normal_at(uint64_t seed, uint32_t e, uint32_t c1, uint32_t c2, uin
   return (e & 1u) ? rad * sin(th) : rad * cos(th);
 }
 
+// Both Box–Muller outputs of the block at c0 (elements 2·c0 and 2·c0+1 of the stream).
+__device__ __forceinline__ void normal_pair(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2,
+                                            uint32_t c3, double& z0, double& z1) {
+  const U4 x = philox4x32(c0, c1, c2, c3, seed);
+  const double u1 = u53(x.x, x.y), u2 = u53(x.z, x.w);
+  const double rad = sqrt(-2.0 * log(u1));
+  double sn, cs;
+  sincos(6.283185307179586 * u2, &sn, &cs);
+  z0 = rad * cs;
+  z1 = rad * sn;
+}
+
+// Global-address-space view of a pointer (global_load/global_store instead of flat_*, which
+// would also count against lgkmcnt and serialise behind LDS traffic).
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gptr(const T* p) {
+  return (const __attribute__((address_space(1))) T*)p;
+}
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr_w(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+
 }  // namespace gpt

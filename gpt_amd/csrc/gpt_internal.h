@@ -26,6 +26,7 @@ struct ChainDesc {
   double* diag;          // (1+D)*steps per-step gradient norms or nullptr
   int32_t* status;       // 0 ok, 1 NaN in geodesic
   uint64_t seed;
+  double epsw, epsU, signal_var, sigma_w;   // per-chain hyper-parameters (sweeps)
 };
 
 struct StepParams {
@@ -34,40 +35,58 @@ struct StepParams {
   long long total_steps;
   int store_every;
   int langevin, stiefel;
-  double signal_var, sigma_w, epsw, epsU;
   const int32_t* I0;              // Q*D 0-based, layout q + Q*k
+  long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
 };
+constexpr int kStamps = 16;       // stamp slots per block
 
 GPT_HD size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// LDS carve of the step kernel (bytes).  Shared by host (size) and device (offsets).
+// LDS carve of the step kernel (bytes), shared by host (size) and device (offsets).
+// Persistent part (whole launch) + a union whose tenants change by phase:
+//   V-phase : temp_l                                     (D·R·MP)
+//   grads   : W_l | U_l | redG                           (R·NP, R·NP, kNW·max(R²,8))
+//   expm    : W_l | expm0 (7·(2R)²) | expm1 (7·R²)       (U_l/redG dead; old U re-read from HBM)
+//   update  : W_l | U_l | redG                           (new U; P5 reads U_l)
 struct StepLayout {
-  int MP, NP;
-  size_t o_temp, o_I, o_w, o_idx, o_y, o_res, o_coef, o_red, o_U, o_W, o_small, bytes;
-  int small_stride;  // doubles per expm scratch matrix
+  int MP, NP, NS, conc;           // NP: n padded to 64 (loop range), NS = NP+1 row stride
+  size_t o_I, o_w, o_idx, o_y, o_res, o_coef, o_gram, o_Ec, o_mx, o_un;
+  size_t o_temp, o_W, o_U, o_red, o_x0, o_x1, bytes;
 };
 
 GPT_HD StepLayout step_layout(int n, int D, int r, int Q, int m) {
   StepLayout L;
-  L.MP = ((m + 7) / 8) * 8 + 1;   // odd (bank spread) and covers the 8-wide unrolled reads
+  L.MP = ((m + 31) / 32) * 32 + 1;   // odd (bank spread); covers 32-wide unrolled reads
   L.NP = ((n + 63) / 64) * 64;
+  L.NS = L.NP + 1;                   // odd stride: rows of U_l/W_l on different banks
   size_t o = 0;
-  L.o_temp = o; o = al16(o + 8 * (size_t)D * r * L.MP);
   L.o_I = o;    o = al16(o + 4 * (size_t)Q * D);
   L.o_w = o;    o = al16(o + 8 * (size_t)Q);
   L.o_idx = o;  o = al16(o + 4 * (size_t)m);
   L.o_y = o;    o = al16(o + 8 * (size_t)m);
-  L.o_res = o;  o = al16(o + 8 * (size_t)m);
+  L.o_res = o;  o = al16(o + 8 * (size_t)L.MP);
   L.o_coef = o; o = al16(o + 8 * (size_t)r * L.MP);
-  L.o_red = o;  o = al16(o + 8 * (size_t)kNW * (1 + r) * 64);
-  L.o_U = o;    o = al16(o + 8 * (size_t)r * L.NP);
-  L.o_W = o;    o = al16(o + 8 * (size_t)r * L.NP);
-  L.o_small = o;
-  const int nn = 2 * r;
-  L.small_stride = nn * nn;
-  // grams (3 r^2) + norms (r) + flag(2) + wave-0 expm scratch (9 nn^2) + wave-1 (9 nn^2)
-  o = al16(o + 8 * (size_t)(3 * r * r + r + 2 + 18 * nn * nn));
-  L.bytes = o;
+  L.o_gram = o; o = al16(o + 8 * (size_t)(3 * r * r + r + 2));
+  L.o_Ec = o;   o = al16(o + 8 * (size_t)(2 * r * r));
+  L.o_mx = o;   o = al16(o + 8 * (size_t)(r * r));
+  L.o_un = o;
+  const size_t nrp = 8 * (size_t)r * L.NS;
+  const size_t red = 8 * (size_t)kNW * (r * r > 8 ? r * r : 8);
+  const size_t x0 = 8 * (size_t)7 * 4 * r * r, x1 = 8 * (size_t)7 * r * r;
+  L.o_temp = o;
+  L.o_W = o;
+  L.o_U = o + nrp;
+  L.o_red = L.o_U + nrp;
+  L.o_x0 = o + nrp;
+  size_t un_v = 8 * (size_t)D * r * L.MP;
+  size_t un_g = 2 * nrp + red;
+  size_t un_xc = nrp + x0 + x1, un_xs = nrp + x0;
+  size_t un = un_v > un_g ? un_v : un_g;
+  L.conc = (al16(o + (un > un_xc ? un : un_xc)) <= 160 * 1024) ? 1 : 0;
+  const size_t ux = L.conc ? un_xc : un_xs;
+  if (ux > un) un = ux;
+  L.o_x1 = L.conc ? L.o_x0 + x0 : L.o_x0;
+  L.bytes = al16(o + un);
   return L;
 }
 

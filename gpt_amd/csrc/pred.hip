@@ -14,13 +14,12 @@ __global__ __launch_bounds__(kNT) void pred_kernel(const double* __restrict__ w,
                                                    double* __restrict__ fhat) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int MP = 65;
-  const int NP = ((n + 63) / 64) * 64;
+  const int NP = ((n + 63) / 64) * 64, NS = NP + 1;
   size_t o = 0;
   double* temp_l = (double*)(smem + o); o = al16(o + 8 * (size_t)D * R * MP);
   int* I_l = (int*)(smem + o);          o = al16(o + 4 * (size_t)Q * D);
   double* w_l = (double*)(smem + o);    o = al16(o + 8 * (size_t)Q);
   int* idx_l = (int*)(smem + o);        o = al16(o + 4 * 64);
-  double* red = (double*)(smem + o);    o = al16(o + 8 * (size_t)kNW * (1 + R) * 64);
   double* U_l = (double*)(smem + o);
   const int tid = threadIdx.x;
   const int s = blockIdx.y;
@@ -28,10 +27,7 @@ __global__ __launch_bounds__(kNT) void pred_kernel(const double* __restrict__ w,
   const int Bt = (int)min((long long)64, Ntest - i0);
   const double* ws = w + (size_t)s * Q;
   const double* Us = U + (size_t)s * n * R * D;
-  for (int x = tid; x < Q * D; x += kNT) {
-    const int q = x / D, kk = x - q * D;
-    I_l[x] = I0[q + Q * kk];
-  }
+  for (int x = tid; x < Q * D; x += kNT) I_l[x] = I0[x];     // transposed: kk*Q + q
   for (int q = tid; q < Q; q += kNT) w_l[q] = ws[q];
   for (int i = tid; i < 64; i += kNT) idx_l[i] = (int)(i0 + min(i, Bt - 1));
   for (int kk = 0; kk < D; ++kk) {
@@ -39,21 +35,16 @@ __global__ __launch_bounds__(kNT) void pred_kernel(const double* __restrict__ w,
     const double* Uk = Us + (size_t)n * R * kk;
     for (int x = tid; x < R * NP; x += kNT) {
       const int l = x / NP, j = x - l * NP;
-      U_l[x] = j < n ? Uk[j + (size_t)n * l] : 0.0;
+      U_l[l * NS + j] = j < n ? Uk[j + (size_t)n * l] : 0.0;
     }
     __syncthreads();
-    phidotU_tile<R>(phitest, (long long)n * kk, (long long)n * D, idx_l, Bt, n, NP, U_l,
+    phidotU_tile<R>(phitest, (long long)n * kk, (long long)n * D, idx_l, Bt, n, NP, NS, U_l,
                     [&](int l, int i, double v) { temp_l[(kk * R + l) * MP + i] = v; });
   }
   __syncthreads();
-  vphase_partials<R>(temp_l, MP, I_l, w_l, Q, D, -1, 0, Bt, red);
-  __syncthreads();
-  if (tid < Bt) {
-    double acc = 0.0;
-#pragma unroll
-    for (int w2 = 0; w2 < kNW; ++w2) acc += red[(w2 * (1 + R)) * 64 + tid];
-    fhat[(size_t)s * Ntest + i0 + tid] = acc;
-  }
+  vphase_tile<R>(temp_l, MP, I_l, w_l, Q, D, 0, Bt, [&](int comp, int i, double v) {
+    if (comp == 0) fhat[(size_t)s * Ntest + i0 + i] = v;
+  });
 }
 
 size_t pred_lds_bytes(int n, int D, int r, int Q) {
@@ -62,8 +53,7 @@ size_t pred_lds_bytes(int n, int D, int r, int Q) {
   o = al16(o + 4 * (size_t)Q * D);
   o = al16(o + 8 * (size_t)Q);
   o = al16(o + 4 * 64);
-  o = al16(o + 8 * (size_t)kNW * (1 + r) * 64);
-  o = al16(o + 8 * (size_t)r * (((n + 63) / 64) * 64));
+  o = al16(o + 8 * (size_t)r * (((n + 63) / 64) * 64 + 1));
   return o;
 }
 

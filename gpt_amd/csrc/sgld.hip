@@ -15,6 +15,15 @@
 
 namespace gpt {
 
+// Diagnostic phase stamps (only when P.stamps != nullptr): thread 0 records s_memtime after
+// the workgroup barrier that closes a phase.
+#define STAMP(slot)                                                                        \
+  do {                                                                                     \
+    if (P.stamps && tid == 0)                                                              \
+      P.stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStamps + (slot)] =         \
+          (long long)__builtin_amdgcn_s_memtime();                                         \
+  } while (0)
+
 template <int R>
 __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
                                                         const ChainDesc* __restrict__ chains,
@@ -30,75 +39,58 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
 
   const int n = P.n, D = P.D, Q = P.Q, m = P.m;
   const StepLayout L = step_layout(n, D, R, Q, m);
-  const int MP = L.MP, NP = L.NP;
-  double* temp_l = (double*)(smem + L.o_temp);
-  int* I_l = (int*)(smem + L.o_I);
+  const int MP = L.MP, NP = L.NP, NS = L.NS;
+  int* IT_l = (int*)(smem + L.o_I);            // I transposed: kk*Q + q
   double* w_l = (double*)(smem + L.o_w);
   int* idx_l = (int*)(smem + L.o_idx);
   double* y_l = (double*)(smem + L.o_y);
   double* res_l = (double*)(smem + L.o_res);
   double* coef_l = (double*)(smem + L.o_coef);
-  double* red = (double*)(smem + L.o_red);
-  double* U_l = (double*)(smem + L.o_U);
+  double* gram = (double*)(smem + L.o_gram);
+  double* Ec = (double*)(smem + L.o_Ec);       // E[:, 0:r] (2r × r)
+  double* mx = (double*)(smem + L.o_mx);       // expm(-t·A) (r × r)
+  double* temp_l = (double*)(smem + L.o_temp);
   double* W_l = (double*)(smem + L.o_W);
-  double* sm = (double*)(smem + L.o_small);
+  double* U_l = (double*)(smem + L.o_U);
+  double* red = (double*)(smem + L.o_red);
 
   const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
   const int start = b * m;
   const int Bt = min(m, P.N - start);
   const int32_t* ord = C.order + (size_t)e * P.N + start;
   const bool wblock = (k == D);
+  STAMP(0);
 
-  // ---- P0: stage temp (this batch), I, w, batch rows/targets, U^(k)
+  // ---- P0: stage temp (this batch), I, w, batch rows and targets
   {
     const double* tsrc = C.temp + (size_t)(t & 1) * D * R * m;
-    for (int o = tid; o < D * R * m; o += kNT) {
-      const int row = o / m, i = o - row * m;
-      temp_l[row * MP + i] = tsrc[o];
+    for (int o = tid; o < D * R * MP; o += kNT) {   // zero tail: unrolled reads run past Bt
+      const int row = o / MP, i = o - row * MP;
+      temp_l[o] = i < Bt ? gptr(tsrc)[row * m + i] : 0.0;
     }
-    for (int o = tid; o < Q * D; o += kNT) {
-      const int q = o / D, kk = o - q * D;
-      I_l[o] = P.I0[q + Q * kk];
-    }
+    for (int i = tid; i < MP; i += kNT) res_l[i] = 0.0;
+    for (int o = tid; o < Q * D; o += kNT) IT_l[o] = gptr(P.I0)[o];   // I0 is already q + Q*k
     const double* wsrc = C.w + (size_t)(t & 1) * Q;
-    for (int q = tid; q < Q; q += kNT) w_l[q] = wsrc[q];
+    for (int q = tid; q < Q; q += kNT) w_l[q] = gptr(wsrc)[q];
     for (int i = tid; i < Bt; i += kNT) {
-      const int row = ord[i];
+      const int row = gptr(ord)[i];
       idx_l[i] = row;
-      y_l[i] = C.y[row];
+      y_l[i] = gptr(C.y)[row];
     }
     for (int o = tid; o < R * MP; o += kNT) coef_l[o] = 0.0;
-    if (!wblock) {
-      const double* Uk = C.U + (size_t)n * R * k;
-      for (int o = tid; o < R * NP; o += kNT) {
-        const int l = o / NP, j = o - l * NP;
-        U_l[o] = j < n ? Uk[j + (size_t)n * l] : 0.0;
-        W_l[o] = 0.0;
-      }
-    }
   }
   __syncthreads();
+  STAMP(1);
 
   // ---- P1: V, fhat, residual, A[:,k,:] (GPT_SGLD.jl:384-399)
-  const int kown = wblock ? -1 : k;
-  const double cN = (double)P.N / (double)Bt;
-  for (int ic = 0; ic < Bt; ic += 64) {
-    vphase_partials<R>(temp_l, MP, I_l, w_l, Q, D, kown, ic, Bt, red);
-    __syncthreads();
-    const int ncomp = wblock ? 1 : (1 + R);
-    for (int o = tid; o < ncomp * 64; o += kNT) {
-      const int comp = o >> 6, ln = o & 63, i = ic + ln;
-      double s = 0.0;
-#pragma unroll
-      for (int w2 = 0; w2 < kNW; ++w2) s += red[(w2 * (1 + R) + comp) * 64 + ln];
-      if (i < Bt) {
-        if (comp == 0) res_l[i] = y_l[i] - s;
-        else coef_l[(comp - 1) * MP + i] = s;
-      }
-    }
-    __syncthreads();
-  }
+  vphase_tile<R>(temp_l, MP, IT_l, w_l, Q, D, wblock ? 0 : k, Bt, [&](int comp, int i, double v) {
+    if (comp == 0) res_l[i] = y_l[i] - v;
+    else coef_l[(comp - 1) * MP + i] = v;
+  });
+  __syncthreads();
+  STAMP(2);
 
+  const double cN = (double)P.N / (double)Bt;
   const long long post = t - P.burnin_steps;
   const bool store = post >= 0 && ((post + 1) % P.store_every) == 0;
   const long long slot = store ? (post + 1) / P.store_every - 1 : 0;
@@ -106,61 +98,88 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
   if (wblock) {
     // ---- gradw and the Langevin step on w (GPT_SGLD.jl:393, 411-414)
     double gn2 = 0.0;
-    const double inv_sw2 = 1.0 / (P.sigma_w * P.sigma_w);
-    const double sqe = sqrt(P.epsw);
+    const double inv_sw2 = 1.0 / (C.sigma_w * C.sigma_w);
+    const double sqe = sqrt(C.epsw);
     for (int q = tid; q < Q; q += kNT) {
-      int Iq[kDMax];
-#pragma unroll
-      for (int kk = 0; kk < kDMax; ++kk) Iq[kk] = kk < D ? I_l[q * D + kk] : 0;
       double g = 0.0;
-      for (int i = 0; i < Bt; ++i) {
-        double v = 1.0;
+      for (int i0 = 0; i0 < Bt; i0 += 16) {
+        double vv[16];
 #pragma unroll
-        for (int kk = 0; kk < kDMax; ++kk)
-          if (kk < D) v *= temp_l[(kk * R + Iq[kk]) * MP + i];
-        g = fma(v, res_l[i], g);
+        for (int u = 0; u < 16; ++u) vv[u] = 1.0;
+        for (int kk = 0; kk < D; ++kk) {
+          const double* row = temp_l + (kk * R + IT_l[kk * Q + q]) * MP + i0;
+#pragma unroll
+          for (int u = 0; u < 16; ++u) vv[u] *= row[u];      // MP covers i0+15 (zero tail)
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) g = fma(vv[u], res_l[i0 + u], g);   // res zero-padded
       }
       const double wq = w_l[q];
-      const double gradw = cN * g / P.signal_var - wq * inv_sw2;
-      double step = P.epsw * gradw / 2;
+      const double gradw = cN * g / C.signal_var - wq * inv_sw2;
+      double step = C.epsw * gradw / 2;
       if (P.langevin) step += sqe * normal_at(C.seed, (uint32_t)q, (uint32_t)t, kWNoise, 0);
       const double wn = wq + step;
-      C.w[(size_t)((t + 1) & 1) * Q + q] = wn;
-      if (store && C.w_store) C.w_store[(size_t)slot * Q + q] = wn;
+      gptr_w(C.w)[(size_t)((t + 1) & 1) * Q + q] = wn;
+      if (store && C.w_store) gptr_w(C.w_store)[(size_t)slot * Q + q] = wn;
       gn2 = fma(gradw, gradw, gn2);
     }
+    __syncthreads();
+    STAMP(3);
     if (C.diag) {
-      const double tot = blk_sum(gn2, red);
+      __syncthreads();
+      const double tot = blk_sum(gn2, red);     // temp_l is dead after the barrier
       if (tid == 0) C.diag[(size_t)t * (1 + D)] = sqrt(tot);
     }
     return;
   }
 
-  // coef[l][i] = A[l][i]·res[i]
+  // coef[l][i] = A[l][i]·res[i]; stage U^(k) (the union slot of temp_l is free now)
   for (int o = tid; o < R * Bt; o += kNT) {
     const int l = o / Bt, i = o - l * Bt;
     coef_l[l * MP + i] *= res_l[i];
   }
+  const double* Ug = C.U + (size_t)n * R * k;
+  for (int o = tid; o < R * NP; o += kNT) {
+    const int l = o / NP, j = o - l * NP;
+    U_l[l * NS + j] = j < n ? gptr(Ug)[j + (size_t)n * l] : 0.0;
+    W_l[l * NS + j] = 0.0;
+  }
   __syncthreads();
+  STAMP(3);
 
   // ---- P2: gradU^(k) = (N/B)/σ² Σ_i phi[:,k,i] (A[:,k,i] res_i)ᵀ   (GPT_SGLD.jl:396-408)
-  const double cU = cN / P.signal_var;
-  const double sq = sqrt(P.epsU);
+  const double cU = cN / C.signal_var;
+  const double sq = sqrt(C.epsU);
   const long long koff = (long long)n * k, rstride = (long long)n * D;
   double gn2 = 0.0;
   for (int j = tid; j < n; j += kNT) {
     double acc[R];
 #pragma unroll
     for (int l = 0; l < R; ++l) acc[l] = 0.0;
-    for (int i0 = 0; i0 < Bt; i0 += 8) {
-      double p[8];
+    double xi[R];
+    for (int i0 = 0; i0 < Bt; i0 += 32) {
+      double p[32];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 32; ++u) {
         const int i = min(i0 + u, Bt - 1);
-        p[u] = C.phi[koff + (long long)uni(idx_l[i]) * rstride + j];
+        p[u] = gptr(C.phi)[koff + (long long)uni(idx_l[i]) * rstride + j];
+      }
+      if (i0 == 0) {   // Langevin noise (ALU) while the loads are in flight
+        // U-noise contract: ξ[j,l] = element l + RE·j of stream (t, U_NOISE, k), RE = R rounded
+        // up to even, so one Box–Muller pair serves (l, l+1) of the same row j.
+        constexpr int RE = R + (R & 1);
+#pragma unroll
+        for (int l = 0; l < R; l += 2) {
+          double z0 = 0.0, z1 = 0.0;
+          if (P.langevin)
+            normal_pair(C.seed, (uint32_t)((l + RE * j) >> 1), (uint32_t)t, kUNoise, (uint32_t)k,
+                        z0, z1);
+          xi[l] = z0;
+          if (l + 1 < R) xi[l + 1] = z1;
+        }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < 32; ++u)
 #pragma unroll
         for (int l = 0; l < R; ++l) acc[l] = fma(p[u], coef_l[l * MP + i0 + u], acc[l]);
     }
@@ -168,13 +187,11 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
     for (int l = 0; l < R; ++l) {
       const double G = acc[l] * cU;
       gn2 = fma(G, G, gn2);
-      const double xi = P.langevin
-          ? normal_at(C.seed, (uint32_t)(j + n * l), (uint32_t)t, kUNoise, (uint32_t)k) : 0.0;
       if (P.stiefel) {
-        W_l[l * NP + j] = sq * G / 2 + xi;                      // :420 drive
+        W_l[l * NS + j] = sq * G / 2 + xi[l];                   // :420 drive
       } else {                                                   // :426 / :437
-        const double u = U_l[l * NP + j];
-        U_l[l * NP + j] = u + (P.epsU * (G - n * u) / 2 + sq * xi);
+        const double u = U_l[l * NS + j];
+        U_l[l * NS + j] = u + (C.epsU * (G - n * u) / 2 + sq * xi[l]);
       }
     }
   }
@@ -183,34 +200,38 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
     if (tid == 0) C.diag[(size_t)t * (1 + D) + 1 + k] = sqrt(tot);
   }
   __syncthreads();
+  STAMP(4);
 
   if (P.stiefel) {
-    double* Mg = sm;              // r×r   Uᵀ·drive
-    double* Ag = sm + R * R;      // r×r   Uᵀ·mom
-    double* Sg = sm + 2 * R * R;  // r×r   momᵀ·mom
-    double* nrm = sm + 3 * R * R; // r
-    int* flag = (int*)(sm + 3 * R * R + R);
-    double* X0 = sm + 3 * R * R + R + 2;       // wave-0 expm region (9·(2r)² doubles)
-    double* X1 = X0 + 9 * (4 * R * R);         // wave-1 expm region
+    double* Mg = gram;              // r×r   Uᵀ·drive
+    double* Ag = gram + R * R;      // r×r   Uᵀ·mom
+    double* Sg = gram + 2 * R * R;  // r×r   momᵀ·mom
+    double* nrm = gram + 3 * R * R; // r
+    int* flag = (int*)(gram + 3 * R * R + R);
     // ---- proj (GPT_SGLD.jl:14-16): mom = V − U(UᵀV + VᵀU)/2
-    blk_gram<R>(U_l, W_l, NP, n, 0, Mg, red);
+    blk_gram<R>(U_l, W_l, NS, n, 0, Mg, red);
     for (int j = tid; j < n; j += kNT) {
       double vj[R], uj[R];
 #pragma unroll
-      for (int l = 0; l < R; ++l) { vj[l] = W_l[l * NP + j]; uj[l] = U_l[l * NP + j]; }
+      for (int l = 0; l < R; ++l) { vj[l] = W_l[l * NS + j]; uj[l] = U_l[l * NS + j]; }
 #pragma unroll
       for (int bb = 0; bb < R; ++bb) {
         double s = 0.0;
 #pragma unroll
         for (int a = 0; a < R; ++a) s = fma(uj[a], Mg[a * R + bb] + Mg[bb * R + a], s);
-        W_l[bb * NP + j] = vj[bb] - s / 2;
+        W_l[bb * NS + j] = vj[bb] - s / 2;
       }
     }
     __syncthreads();
-    // ---- geod (GPT_SGLD.jl:19-37)
-    blk_gram<R>(U_l, W_l, NP, n, 1, Ag, red);   // Ag, then Sg right after it
+    STAMP(5);
+    // ---- geod (GPT_SGLD.jl:19-37): A = Uᵀmom, S = momᵀmom
+    blk_gram<R>(U_l, W_l, NS, n, 0, Ag, red);
+    blk_gram<R>(W_l, W_l, NS, n, 0, Sg, red);
+    STAMP(6);
     const double tt = sq;
     const int nn = 2 * R;
+    double* X0 = (double*)(smem + L.o_x0);     // U_l / red are dead from here to the update
+    double* X1 = (double*)(smem + L.o_x1);
     if (wv == 0) {
       for (int o = tid; o < nn * nn; o += 64) {
         const int i = o / nn, j = o - i * nn;
@@ -220,48 +241,56 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
         X0[o] = tt * v;
       }
       wave_sync();
-      const bool bad = wave_expm(X0, nn);
+      const bool bad = wave_expm<2 * R>(X0);
+      for (int o = tid; o < nn * R; o += 64) {
+        const int a = o / R, l = o - a * R;
+        Ec[o] = X0[nn * nn + a * nn + l];
+      }
       if (tid == 0) flag[0] = bad ? 1 : 0;
-    } else if (wv == 1) {
-      const int ln = tid - 64;
+      wave_sync();
+    }
+    if (wv == (L.conc ? 1 : 0)) {
+      const int ln = tid & 63;
       for (int o = ln; o < R * R; o += 64) X1[o] = -tt * Ag[o];
       wave_sync();
-      wave_expm(X1, R);
+      wave_expm<R>(X1);
+      for (int o = ln; o < R * R; o += 64) mx[o] = X1[R * R + o];
     }
     __syncthreads();
+    STAMP(7);
     if (flag[0]) {
       if (tid == 0) __hip_atomic_store(C.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
-    const double* E = X0 + 8 * nn * nn;     // 2r×2r, use columns 0..r-1
-    const double* mexp = X1 + 8 * R * R;    // r×r
+    // tmpU = ([U mom]·E[:,1:r])·expm(-tA)   (old U re-read from HBM/L2; mom in W_l)
     for (int j = tid; j < n; j += kNT) {
       double x[2 * R];
 #pragma unroll
-      for (int l = 0; l < R; ++l) { x[l] = U_l[l * NP + j]; x[R + l] = W_l[l * NP + j]; }
+      for (int l = 0; l < R; ++l) { x[l] = gptr(Ug)[j + (size_t)n * l]; x[R + l] = W_l[l * NS + j]; }
       double row1[R];
 #pragma unroll
       for (int l = 0; l < R; ++l) {
         double s = 0.0;
 #pragma unroll
-        for (int a = 0; a < 2 * R; ++a) s = fma(x[a], E[a * nn + l], s);
+        for (int a = 0; a < 2 * R; ++a) s = fma(x[a], Ec[a * R + l], s);
         row1[l] = s;
       }
 #pragma unroll
       for (int l = 0; l < R; ++l) {
         double s = 0.0;
 #pragma unroll
-        for (int c2 = 0; c2 < R; ++c2) s = fma(row1[c2], mexp[c2 * R + l], s);
-        W_l[l * NP + j] = s;
+        for (int c2 = 0; c2 < R; ++c2) s = fma(row1[c2], mx[c2 * R + l], s);
+        W_l[l * NS + j] = s;
       }
     }
     __syncthreads();
-    blk_gram<R>(W_l, W_l, NP, n, 2, nrm, red);
-    for (int o = tid; o < R * n; o += kNT) {
-      const int l = o / n, j = o - l * n;
-      U_l[l * NP + j] = W_l[l * NP + j] / sqrt(nrm[l]);
+    blk_gram<R>(W_l, W_l, NS, n, 2, nrm, red);
+    for (int o = tid; o < R * NP; o += kNT) {
+      const int l = o / NP, j = o - l * NP;
+      U_l[l * NS + j] = j < n ? W_l[l * NS + j] / sqrt(nrm[l]) : 0.0;
     }
     __syncthreads();
+    STAMP(8);
   }
 
   // ---- write U^(k) (and the sample store, GPT_SGLD.jl:441-444)
@@ -270,9 +299,9 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
     double* Us = (store && C.U_store) ? C.U_store + ((size_t)slot * D + k) * n * R : nullptr;
     for (int o = tid; o < R * n; o += kNT) {
       const int l = o / n, j = o - l * n;
-      const double u = U_l[l * NP + j];
-      Uk[o] = u;
-      if (Us) Us[o] = u;
+      const double u = U_l[l * NS + j];
+      gptr_w(Uk)[o] = u;
+      if (Us) gptr_w(Us)[o] = u;
     }
   }
 
@@ -283,11 +312,15 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
     const int s1 = b1 * m;
     const int B1 = min(m, P.N - s1);
     const int32_t* ord1 = C.order + (size_t)e1 * P.N + s1;
-    for (int i = tid; i < B1; i += kNT) idx_l[i] = ord1[i];
     __syncthreads();
+    for (int i = tid; i < B1; i += kNT) idx_l[i] = gptr(ord1)[i];
+    __syncthreads();
+    STAMP(9);
     double* tdst = C.temp + (size_t)(t1 & 1) * D * R * m + (size_t)k * R * m;
-    phidotU_tile<R>(C.phi, koff, rstride, idx_l, B1, n, NP, U_l,
-                    [&](int l, int i, double v) { tdst[l * m + i] = v; });
+    phidotU_tile<R>(C.phi, koff, rstride, idx_l, B1, n, NP, NS, U_l,
+                    [&](int l, int i, double v) { gptr_w(tdst)[l * m + i] = v; });
+    __syncthreads();
+    STAMP(10);
   }
 }
 
@@ -303,7 +336,7 @@ __global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
   if (t >= P.total_steps) return;
   const int n = P.n, D = P.D, m = P.m;
   const StepLayout L = step_layout(n, D, R, P.Q, m);
-  const int NP = L.NP;
+  const int NP = L.NP, NS = L.NS;
   int* idx_l = (int*)(smem + L.o_idx);
   double* U_l = (double*)(smem + L.o_U);
   const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
@@ -314,11 +347,11 @@ __global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
   const double* Uk = C.U + (size_t)n * R * k;
   for (int o = tid; o < R * NP; o += kNT) {
     const int l = o / NP, j = o - l * NP;
-    U_l[o] = j < n ? Uk[j + (size_t)n * l] : 0.0;
+    U_l[l * NS + j] = j < n ? Uk[j + (size_t)n * l] : 0.0;
   }
   __syncthreads();
   double* tdst = C.temp + (size_t)(t & 1) * D * R * m + (size_t)k * R * m;
-  phidotU_tile<R>(C.phi, (long long)n * k, (long long)n * D, idx_l, Bt, n, NP, U_l,
+  phidotU_tile<R>(C.phi, (long long)n * k, (long long)n * D, idx_l, Bt, n, NP, NS, U_l,
                   [&](int l, int i, double v) { tdst[l * m + i] = v; });
 }
 

@@ -56,6 +56,10 @@ class SGLDSession:
         self.total_steps = total if max_steps <= 0 else min(total, max_steps)
         self.nstore = (maxepoch * self.numbatches) // store_every
 
+    def set_hyper(self, chain, epsw, epsU, signal_var, sigma_w=1.0):
+        check(lib().gpt_sgld_session_set_hyper(self._h, chain, float(epsw), float(epsU),
+                                               float(signal_var), float(sigma_w)))
+
     def run(self, nsteps):
         check(lib().gpt_sgld_session_run(self._h, int(nsteps)))
 

@@ -91,6 +91,10 @@ int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchains, const u
                             const double* const* phi_dev, const double* const* y_dev,
                             const int32_t* I_host, int32_t store_on_device, void* hip_stream,
                             gpt_sgld_session** out);
+/* Per-chain step sizes / variances (a hyper-parameter sweep, kin40kExperiment.jl:67-74);
+ * call before the first run. */
+int gpt_sgld_session_set_hyper(gpt_sgld_session* s, int32_t chain, double epsw, double epsU,
+                               double signal_var, double sigma_w);
 /* Queue `nsteps` SGLD steps of every chain on the session stream (asynchronous). */
 int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps);
 int gpt_sgld_session_sync(gpt_sgld_session* s);
@@ -101,6 +105,9 @@ int64_t gpt_sgld_session_steps_done(gpt_sgld_session* s);
 /* Run `nsteps` steps WITHOUT graph capture, bracketing every step-kernel launch with hipEvents;
  * *avg_us = mean step-kernel duration (the roofline's per-launch time).  Synchronises. */
 int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, double* avg_us);
+/* Diagnostic: run nsteps un-captured steps recording s_memtime (shader-clock ticks)
+ * stamps per phase; out = nsteps x (D+1)*nchains x 16 int64 (0 = phase not reached). */
+int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out);
 /* Copy chain c's stores / status back (status: GPT_OK or GPT_ERR_NAN_GEODESIC). */
 int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double* w_store, double* U_store,
                            double* diag, int32_t* status);
@@ -130,6 +137,8 @@ int gpt_gpnt_sgld(const double* phi, const double* y, int64_t n, int64_t N, doub
                   int64_t burnin, int64_t maxepoch, uint64_t seed, double* theta_store);
 
 const char* gpt_last_error(void);
+/* LDS bytes one step workgroup needs for this shape (must be <= 163840). */
+int64_t gpt_sgld_lds_bytes(int64_t n, int64_t D, int64_t r, int64_t Q, int64_t m);
 int gpt_device_count(void);
 
 #ifdef __cplusplus

@@ -286,6 +286,14 @@ def stiefel_init(Zr_n):
     return Z.T @ inv_sqrt
 
 
+def u_noise(n, r, seed, step, k):
+    """U-noise contract: ξ[j, l] = element l + RE·j of stream (step, U_NOISE, k), RE = r rounded
+    up to even (one Box–Muller pair serves columns (l, l+1) of a row).  Stands in for Julia's
+    ``randn(n, r)`` at GPT_SGLD.jl:420 / ``randn(n, r, D)`` at :426."""
+    re = r + (r & 1)
+    return px.normals(re * n, seed, step, px.U_NOISE, k).reshape((n, re))[:, :r]
+
+
 def init_state(n, r, D, Q, seed, stiefel=True, sigma_w=1.0):
     """GPT_SGLD.jl:357-369 on the framework streams: w = σ_w·randn(Q); U_k polar factor of
     Z = randn(r, n) (Stiefel) or randn(n,r)/sqrt(n) (non-Stiefel)."""
@@ -346,7 +354,7 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
                 w = w + epsw * g["gradw"] / 2
             if stiefel:
                 for k in range(D):
-                    xi = px.normals(n * r, param_seed, step, px.U_NOISE, k).reshape((n, r), order="F")
+                    xi = u_noise(n, r, param_seed, step, k)
                     drive = math.sqrt(epsU) * g["gradU"][:, :, k] / 2
                     mom = proj(U[:, :, k], drive + xi if langevin else drive)
                     Un, ok = geod(U[:, :, k], mom, math.sqrt(epsU))
@@ -357,8 +365,7 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
             else:
                 upd = epsU * (g["gradU"] - n * U) / 2
                 if langevin:
-                    xi = np.stack([px.normals(n * r, param_seed, step, px.U_NOISE, k).reshape((n, r), order="F")
-                                   for k in range(D)], axis=2)
+                    xi = np.stack([u_noise(n, r, param_seed, step, k) for k in range(D)], axis=2)
                     upd = upd + math.sqrt(epsU) * xi
                 U = U + upd
             if epoch > burnin:

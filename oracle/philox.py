@@ -16,6 +16,7 @@ reference one for one (SURVEY.md §8(a) "RNG consumption order"):
     PERM          (i,    epoch,  PERM,    0)           randperm(N)           :373
     W_NOISE       (e>>1, step,   W_NOISE, 0)           randn(Q)              :412
     U_NOISE       (e>>1, step,   U_NOISE, k)           randn(n, r)           :420
+                  element e = l + RE·j for ξ[j,l], RE = r rounded up to even
     THETA_INIT    (e>>1, 0,      TH_INIT, 0)           theta = randn(n)      :815
     THETA_NOISE   (e>>1, t,      TH_NOISE,0)           randn(n)              :836
 

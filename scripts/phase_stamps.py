@@ -1,0 +1,70 @@
+"""Per-phase timing of sgld_step_kernel from in-kernel s_memtime stamps (diagnostic build path:
+stamps are written only by gpt_sgld_session_stamps launches).  Usage on the GPU box:
+    python scripts/phase_stamps.py [--chains C] [--steps S]
+"""
+import argparse
+import ctypes as C
+import math
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+NAMES = {1: "P0 stage", 2: "P1 V-phase", 3: "w-block gradw / U stage", 4: "P2 gradU+noise",
+         5: "proj gram+mom", 6: "geod grams", 7: "expm x2", 8: "tmpU+norm", 9: "U write+idx",
+         10: "P5 next temp"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chains", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--n", type=int, default=500)
+    ap.add_argument("--r", type=int, default=5)
+    ap.add_argument("--m", type=int, default=50)
+    args = ap.parse_args()
+    import torch
+    import bench
+    from gpt_amd import GPT_SGLD as G
+    from gpt_amd._lib import check, lib
+    from gpt_amd.session import SGLDSession, feature_device
+    dev = torch.device("cuda", 0)
+    n, D, r, Q, m = args.n, 8, args.r, 200, args.m
+    Xtr, ytr, _, _, _ = bench.kin40k(D)
+    ls = np.array([2.5242, 2.3376, 1.3630, 1.4949, 1.6022, 1.1366, 1.1964, 1.7028])
+    I = G.samplenz(r, D, Q, 17)
+    Z, b = G.feature_inputs(n, D, 17)
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    phi = feature_device(tt(Xtr.T), tt(ls), 1.042, math.sqrt(n / Q ** (1 / D)), tt(Z.T), tt(b.T))
+    y = tt(ytr)
+    s = SGLDSession(phi, y, I, r, Q, m, 1e-5, 1e-8, 0.0476, 0, 3, list(range(1, args.chains + 1)),
+                    store=False)
+    s.run(50)
+    s.sync()
+    nb = (D + 1) * args.chains
+    out = np.zeros((args.steps, nb, 16), dtype=np.int64)
+    check(lib().gpt_sgld_session_stamps(s._h, args.steps, out.ctypes.data_as(C.POINTER(C.c_int64))))
+    kblocks = out.reshape(args.steps, args.chains, D + 1, 16)[:, :, :D, :]
+    wblocks = out.reshape(args.steps, args.chains, D + 1, 16)[:, :, D, :]
+    print("k-blocks: median cycles per phase (stamp[i] - stamp[i-1])")
+    prev = 0
+    tot = np.median((kblocks[..., 10] - kblocks[..., 0]).ravel())
+    for i in range(1, 11):
+        d = kblocks[..., i] - kblocks[..., prev]
+        ok = kblocks[..., i] > 0
+        if ok.any():
+            v = np.median(d[ok])
+            print("  %2d %-26s %8.0f cyc  %5.1f%%" % (i, NAMES[i], v, 100 * v / tot))
+            prev = i
+    print("  total k-block %.0f cycles" % tot)
+    dw = np.median((wblocks[..., 3] - wblocks[..., 0]).ravel())
+    print("w-block total %.0f cycles (V-phase %.0f)" % (dw, np.median((wblocks[..., 2] - wblocks[..., 0]).ravel())))
+    t_us = s.time_steps(20)
+    print("event-timed step kernel: %.2f us" % t_us)
+
+
+if __name__ == "__main__":
+    main()

@@ -3,7 +3,7 @@ Philox streams and permutations.
 
 Tolerances (fp64 path; the GPU sums in a different order and uses leave-one-out products
 instead of computeU_phi's division, GPT_SGLD.jl:253):
-  features                       max |Δ| <= 4e-16·|c|  (cos differs by ≤ 1 ulp between libms)
+  features                       max |Δ| <= 1e-14·|c|  (same argument bits; libm cos differs by a few ulp)
   pred / fhat                    max |Δ| <= 1e-12·max|f|
   sampler trajectories           max |Δ| <= 1e-8·max|x| over every stored w and U sample
   per-step gradient norms        relative <= 1e-9
@@ -52,7 +52,7 @@ def test_feature_matches_oracle():
     got = G().feature(X, ls, 1.3, 2.0, Z, b)
     want = R.feature(X, ls, 1.3, 2.0, Z, b)
     assert got.shape == (n, D, N)
-    assert np.abs(got - want).max() <= 4e-16 * np.abs(want).max() * 4
+    assert np.abs(got - want).max() <= 1e-14 * np.abs(want).max()
 
 
 def test_feature_seeded_generation_c():
@@ -106,6 +106,8 @@ CASES = {
     "kin40k_shape": (500, 8, 200, 5, 200, 50, 0, 1, 1, True, True),
     "wide_batch": (64, 4, 300, 4, 30, 100, 0, 1, 1, True, True),
     "rank10": (100, 4, 120, 10, 60, 30, 0, 1, 1, True, True),
+    "ref_kin40k_rank20": (150, 8, 100, 20, 200, 50, 0, 1, 1, True, True),
+    "batch256": (96, 4, 600, 5, 80, 256, 0, 1, 1, True, True),
 }
 
 
