@@ -28,7 +28,7 @@ __device__ __forceinline__ double wave_max(double v) {
 // Sum of one value per thread over the workgroup; every thread gets the total.
 // Uses red[0..kNW); deterministic order.
 __device__ __forceinline__ double blk_sum(double v, double* red) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   v = wave_sum(v);
   if (lane == 0) red[wv] = v;
   __syncthreads();
@@ -76,25 +76,36 @@ struct RCfg {
 };
 
 // temp[l][i] = Σ_j phi[koff + row(i)*rstride + j] · U_l[l*NP + j]   (GPT_SGLD.jl:193-205)
-// for i < Bt, row(i) = idx_l[i].  Lanes stride over j (coalesced 512-B loads), wave w takes
+// for i < Bt (rows from ordp, see batch_rows_lane).  Lanes stride over j (coalesced 512-B loads), wave w takes
 // columns i = base + w + kNW·ii; partials are combined with one Butterfly per pass.
 // U_l rows (stride NS) must be zero-padded for j in [n, NP).
+// Row of batch column (base + lane) for every lane: one coalesced load per 64 columns; single
+// rows are then broadcast with v_readlane (no per-column memory round trip).  ordp == nullptr
+// means the identity map row = rowbase + column (prediction over a contiguous test range).
+__device__ __forceinline__ int batch_rows_lane(const int32_t* ordp, int rowbase, int base, int Bt) {
+  const int lane = threadIdx.x & 63;
+  const int i = min(base + lane, Bt - 1);
+  return ordp ? gptr(ordp)[i] : rowbase + i;
+}
+
 template <int R, class Out>
 __device__ __forceinline__ void phidotU_tile(const double* __restrict__ phi, long long koff,
-                                             long long rstride, const int* idx_l, int Bt,
-                                             int n, int NP, int NS, const double* U_l, Out out) {
+                                             long long rstride, const int32_t* ordp, int rowbase,
+                                             int Bt, int n, int NP, int NS, const double* U_l,
+                                             Out out) {
   using C = RCfg<R>;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   constexpr int SH = 6 - Butterfly<C::NV>::P;
   for (int base = 0; base < Bt; base += kNW * C::ICH) {
     double v[C::NV];
 #pragma unroll
     for (int u = 0; u < C::NV; ++u) v[u] = 0.0;
+    const int vrow = batch_rows_lane(ordp, rowbase, base, Bt);   // kNW·ICH <= 64 columns
     const __attribute__((address_space(1))) double* rowp[C::ICH];
 #pragma unroll
     for (int ii = 0; ii < C::ICH; ++ii) {
-      const int i = min(base + wv + kNW * ii, Bt - 1);
-      rowp[ii] = gptr(phi) + koff + (long long)uni(idx_l[i]) * rstride;
+      const int c = min(wv + kNW * ii, 63);
+      rowp[ii] = gptr(phi) + koff + (long long)__builtin_amdgcn_readlane(vrow, c) * rstride;
     }
     const int JS = NP >> 6;
 #pragma unroll 4
@@ -129,13 +140,19 @@ __device__ __forceinline__ void phidotU_tile(const double* __restrict__ phi, lon
 //              division of computeU_phi — a leave-one-out product)
 // reduced over q by one Butterfly per pass (no cross-wave traffic).  IT_l is I transposed
 // (kk·Q + q, conflict-free per-lane reads).  out(comp, i, value) is called once per value.
-template <int R, class Out>
+template <int R>
+struct VCfg {
+  static constexpr int NC = 1 + R;
+  static constexpr int ICV_MAX = (64 / NC) < 12 ? (64 / NC) : 12;   // columns per wave pass
+  static constexpr int ICV_SMALL = ICV_MAX < 7 ? ICV_MAX : 7;      // batches <= 56 in one pass
+};
+
+template <int R, int ICV, class Out>
 __device__ __forceinline__ void vphase_tile(const double* temp_l, int MP, const int* IT_l,
                                             const double* w_l, int Q, int D, int kown, int Bt,
                                             Out out) {
   constexpr int NC = 1 + R;
-  constexpr int ICV = (64 / NC) < 12 ? (64 / NC) : 12;   // columns per wave pass
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   for (int base = 0; base < Bt; base += kNW * ICV) {
     const int nii = min(ICV, (Bt - base - wv + kNW - 1) / kNW);
     int col[ICV];
@@ -188,7 +205,7 @@ __device__ __forceinline__ void vphase_tile(const double* temp_l, int MP, const 
 template <int R>
 __device__ __forceinline__ void blk_gram(const double* X, const double* Y, int NP, int n,
                                          int mode, double* out, double* red) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   const int nout = mode == 0 ? R * R : (mode == 1 ? 2 * R * R : R);
   const int chunk = (n + kNW - 1) / kNW;
   const int j0 = wv * chunk, j1 = min(n, j0 + chunk);
@@ -301,6 +318,66 @@ __device__ __forceinline__ void wave_solve(double* M, double* X) {
   wave_sync();
 }
 
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Solve M·X = X0 (X holds X0) for column diagonally dominant M: Gaussian elimination with
+// partial pivoting provably never swaps rows there, so the arithmetic of wave_solve is
+// reproduced without the pivot searches.  Lanes own columns of [M | X] in registers; pivot
+// rows and multipliers are broadcast with v_readlane (no LDS round trips).  Returns false
+// (nothing written) when M is not diagonally dominant — the caller then pivots.
+template <int NN>
+__device__ __forceinline__ bool wave_solve_dd(const double* M, double* X) {
+  const int lane = threadIdx.x & 63;
+  bool dd = true;
+  if (lane < NN) {
+    double off = 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+      if (i != lane) off += fabs(M[i * NN + lane]);
+    dd = fabs(M[lane * NN + lane]) > off;
+  }
+  if (!__all(dd)) return false;
+  double col[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    const int c = lane < NN ? lane : lane - NN;
+    col[i] = lane < NN ? M[i * NN + c] : (lane < 2 * NN ? X[i * NN + c] : 0.0);
+  }
+#pragma unroll
+  for (int p = 0; p < NN; ++p) {              // forward elimination (getrf + L solve)
+    const double rp = 1.0 / readlane_d(col[p], p);
+#pragma unroll
+    for (int i = p + 1; i < NN; ++i) {
+      const double f = readlane_d(col[i], p) * rp;
+      col[i] -= f * col[p];
+    }
+  }
+  const bool xl = lane >= NN;                 // only the right-hand-side lanes back-substitute
+#pragma unroll
+  for (int k = NN - 1; k >= 0; --k) {         // back substitution, column-oriented (trsm)
+    double u[NN];
+#pragma unroll
+    for (int i = 0; i <= k; ++i) u[i] = readlane_d(col[i], k);   // U[0..k][k] from lane k
+    if (xl) {
+      col[k] = col[k] / u[k];
+#pragma unroll
+      for (int i = 0; i < k; ++i) col[i] -= col[k] * u[i];
+    }
+  }
+  wave_sync();
+  if (lane >= NN && lane < 2 * NN) {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) X[i * NN + lane - NN] = col[i];
+  }
+  wave_sync();
+  return true;
+}
+
 // expm(A) for an NN×NN matrix held in S[0..NN²) (row-major; overwritten).  Padé
 // scaling-and-squaring of Julia Base 0.3 expm! (Higham 2005; thresholds 0.015/0.25/0.95/2.1,
 // 13th order above, θ13 = 5.4).  Scratch S: 7 NN² doubles; the result is left at S + NN².
@@ -389,7 +466,9 @@ __device__ bool wave_expm(double* S) {
     X[o] = V[o] + U[o];
   }
   wave_sync();
-  wave_solve<NN>(M, X);
+  bool solved = false;
+  if constexpr (2 * NN <= 64) solved = wave_solve_dd<NN>(M, X);
+  if (!solved) wave_solve<NN>(M, X);
   for (int z = 0; z < si; ++z) {
     wave_mm<NN>(X, X, T);
     for (int o = lane; o < q; o += 64) X[o] = T[o];

@@ -64,6 +64,11 @@ template <class T>
 __device__ __forceinline__ const __attribute__((address_space(1))) T* gptr(const T* p) {
   return (const __attribute__((address_space(1))) T*)p;
 }
+// Constant-address-space view: uniform indices become scalar (s_load) loads.
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* cptr(const T* p) {
+  return (const __attribute__((address_space(4))) T*)p;
+}
 template <class T>
 __device__ __forceinline__ __attribute__((address_space(1))) T* gptr_w(T* p) {
   return (__attribute__((address_space(1))) T*)p;

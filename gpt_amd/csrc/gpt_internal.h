@@ -49,7 +49,7 @@ GPT_HD size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
 //   expm    : W_l | expm0 (7·(2R)²) | expm1 (7·R²)       (U_l/redG dead; old U re-read from HBM)
 //   update  : W_l | U_l | redG                           (new U; P5 reads U_l)
 struct StepLayout {
-  int MP, NP, NS, conc;           // NP: n padded to 64 (loop range), NS = NP+1 row stride
+  int MP, NP, NS, conc, keepU;    // NP: n padded to 64 (loop range), NS = NP+1 row stride
   size_t o_I, o_w, o_idx, o_y, o_res, o_coef, o_gram, o_Ec, o_mx, o_un;
   size_t o_temp, o_W, o_U, o_red, o_x0, o_x1, bytes;
 };
@@ -71,21 +71,30 @@ GPT_HD StepLayout step_layout(int n, int D, int r, int Q, int m) {
   L.o_mx = o;   o = al16(o + 8 * (size_t)(r * r));
   L.o_un = o;
   const size_t nrp = 8 * (size_t)r * L.NS;
-  const size_t red = 8 * (size_t)kNW * (r * r > 8 ? r * r : 8);
+  const size_t red = 8 * (size_t)kNW * (2 * r * r > 8 ? 2 * r * r : 8);
   const size_t x0 = 8 * (size_t)7 * 4 * r * r, x1 = 8 * (size_t)7 * r * r;
   L.o_temp = o;
   L.o_W = o;
   L.o_U = o + nrp;
   L.o_red = L.o_U + nrp;
-  L.o_x0 = o + nrp;
-  size_t un_v = 8 * (size_t)D * r * L.MP;
-  size_t un_g = 2 * nrp + red;
-  size_t un_xc = nrp + x0 + x1, un_xs = nrp + x0;
+  const size_t un_v = 8 * (size_t)D * r * L.MP;
+  const size_t un_g = 2 * nrp + red;
   size_t un = un_v > un_g ? un_v : un_g;
-  L.conc = (al16(o + (un > un_xc ? un : un_xc)) <= 160 * 1024) ? 1 : 0;
-  const size_t ux = L.conc ? un_xc : un_xs;
-  if (ux > un) un = ux;
-  L.o_x1 = L.conc ? L.o_x0 + x0 : L.o_x0;
+  const size_t cap = 160 * 1024;
+  // Preferred: expm scratch after red with U_l kept (old U stays in LDS for tmpU), both expm
+  // concurrent.  Fallbacks alias the scratch over U_l/red, then run the two expm in turn.
+  if (al16(o + (un > 2 * nrp + red + x0 + x1 ? un : 2 * nrp + red + x0 + x1)) <= cap) {
+    L.keepU = 1; L.conc = 1;
+    L.o_x0 = L.o_red + red; L.o_x1 = L.o_x0 + x0;
+    if (2 * nrp + red + x0 + x1 > un) un = 2 * nrp + red + x0 + x1;
+  } else {
+    L.keepU = 0;
+    L.o_x0 = o + nrp;
+    L.conc = (al16(o + (un > nrp + x0 + x1 ? un : nrp + x0 + x1)) <= cap) ? 1 : 0;
+    L.o_x1 = L.conc ? L.o_x0 + x0 : L.o_x0;
+    const size_t ux = L.conc ? nrp + x0 + x1 : nrp + x0;
+    if (ux > un) un = ux;
+  }
   L.bytes = al16(o + un);
   return L;
 }

@@ -38,11 +38,12 @@ __global__ __launch_bounds__(kNT) void pred_kernel(const double* __restrict__ w,
       U_l[l * NS + j] = j < n ? Uk[j + (size_t)n * l] : 0.0;
     }
     __syncthreads();
-    phidotU_tile<R>(phitest, (long long)n * kk, (long long)n * D, idx_l, Bt, n, NP, NS, U_l,
+    phidotU_tile<R>(phitest, (long long)n * kk, (long long)n * D, nullptr, (int)i0, Bt, n, NP, NS,
+                    U_l,
                     [&](int l, int i, double v) { temp_l[(kk * R + l) * MP + i] = v; });
   }
   __syncthreads();
-  vphase_tile<R>(temp_l, MP, I_l, w_l, Q, D, 0, Bt, [&](int comp, int i, double v) {
+  vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, I_l, w_l, Q, D, 0, Bt, [&](int comp, int i, double v) {
     if (comp == 0) fhat[(size_t)s * Ntest + i0 + i] = v;
   });
 }

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const ChainDesc C = chains[blockIdx.y];
   const int k = blockIdx.x;
-  const int tid = threadIdx.x, wv = tid >> 6;
+  const int tid = threadIdx.x, wv = uni(tid >> 6);
   const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
   if (__hip_atomic_load(C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
@@ -82,11 +82,25 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
   __syncthreads();
   STAMP(1);
 
+  const long long koff = (long long)n * k, rstride = (long long)n * D;
+  const long long t1 = t + 1;
+  const int e1 = (int)(t1 / P.nb), b1 = (int)(t1 - (long long)e1 * P.nb);
+  const int s1 = b1 * m;
+  const bool has_next = t1 < P.total_steps;
+  const int B1 = has_next ? min(m, P.N - s1) : 0;
+  const int32_t* ord1 = C.order + (size_t)(has_next ? e1 : e) * P.N + (has_next ? s1 : start);
+
   // ---- P1: V, fhat, residual, A[:,k,:] (GPT_SGLD.jl:384-399)
-  vphase_tile<R>(temp_l, MP, IT_l, w_l, Q, D, wblock ? 0 : k, Bt, [&](int comp, int i, double v) {
-    if (comp == 0) res_l[i] = y_l[i] - v;
-    else coef_l[(comp - 1) * MP + i] = v;
-  });
+  {
+    auto vout = [&](int comp, int i, double v) {
+      if (comp == 0) res_l[i] = y_l[i] - v;
+      else coef_l[(comp - 1) * MP + i] = v;
+    };
+    if (Bt <= kNW * VCfg<R>::ICV_SMALL)
+      vphase_tile<R, VCfg<R>::ICV_SMALL>(temp_l, MP, IT_l, w_l, Q, D, wblock ? 0 : k, Bt, vout);
+    else
+      vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, IT_l, w_l, Q, D, wblock ? 0 : k, Bt, vout);
+  }
   __syncthreads();
   STAMP(2);
 
@@ -150,19 +164,24 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
   // ---- P2: gradU^(k) = (N/B)/σ² Σ_i phi[:,k,i] (A[:,k,i] res_i)ᵀ   (GPT_SGLD.jl:396-408)
   const double cU = cN / C.signal_var;
   const double sq = sqrt(C.epsU);
-  const long long koff = (long long)n * k, rstride = (long long)n * D;
   double gn2 = 0.0;
-  for (int j = tid; j < n; j += kNT) {
+  // Uniform trip count (j clamped, writes masked): every lane takes part in the row-vector
+  // load below, so v_readlane never reads a lane that skipped it.
+  for (int j0 = 0; j0 < n; j0 += kNT) {
+    const int j = j0 + tid;
+    const bool jok = j < n;
+    const int jc = jok ? j : n - 1;
     double acc[R];
 #pragma unroll
     for (int l = 0; l < R; ++l) acc[l] = 0.0;
     double xi[R];
     for (int i0 = 0; i0 < Bt; i0 += 32) {
+      const int vrow = batch_rows_lane(ord, 0, i0, Bt);      // lane u: row of column i0+u
       double p[32];
 #pragma unroll
       for (int u = 0; u < 32; ++u) {
-        const int i = min(i0 + u, Bt - 1);
-        p[u] = gptr(C.phi)[koff + (long long)uni(idx_l[i]) * rstride + j];
+        const int row = __builtin_amdgcn_readlane(vrow, u);  // columns past Bt: clamped row
+        p[u] = (gptr(C.phi) + koff + (long long)row * rstride)[jc];
       }
       if (i0 == 0) {   // Langevin noise (ALU) while the loads are in flight
         // U-noise contract: ξ[j,l] = element l + RE·j of stream (t, U_NOISE, k), RE = R rounded
@@ -172,7 +191,7 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
         for (int l = 0; l < R; l += 2) {
           double z0 = 0.0, z1 = 0.0;
           if (P.langevin)
-            normal_pair(C.seed, (uint32_t)((l + RE * j) >> 1), (uint32_t)t, kUNoise, (uint32_t)k,
+            normal_pair(C.seed, (uint32_t)((l + RE * jc) >> 1), (uint32_t)t, kUNoise, (uint32_t)k,
                         z0, z1);
           xi[l] = z0;
           if (l + 1 < R) xi[l + 1] = z1;
@@ -183,15 +202,17 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
 #pragma unroll
         for (int l = 0; l < R; ++l) acc[l] = fma(p[u], coef_l[l * MP + i0 + u], acc[l]);
     }
+    if (jok) {
 #pragma unroll
-    for (int l = 0; l < R; ++l) {
-      const double G = acc[l] * cU;
-      gn2 = fma(G, G, gn2);
-      if (P.stiefel) {
-        W_l[l * NS + j] = sq * G / 2 + xi[l];                   // :420 drive
-      } else {                                                   // :426 / :437
-        const double u = U_l[l * NS + j];
-        U_l[l * NS + j] = u + (C.epsU * (G - n * u) / 2 + sq * xi[l]);
+      for (int l = 0; l < R; ++l) {
+        const double G = acc[l] * cU;
+        gn2 = fma(G, G, gn2);
+        if (P.stiefel) {
+          W_l[l * NS + j] = sq * G / 2 + xi[l];                  // :420 drive
+        } else {                                                  // :426 / :437
+          const double u = U_l[l * NS + j];
+          U_l[l * NS + j] = u + (C.epsU * (G - n * u) / 2 + sq * xi[l]);
+        }
       }
     }
   }
@@ -225,8 +246,7 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
     __syncthreads();
     STAMP(5);
     // ---- geod (GPT_SGLD.jl:19-37): A = Uᵀmom, S = momᵀmom
-    blk_gram<R>(U_l, W_l, NS, n, 0, Ag, red);
-    blk_gram<R>(W_l, W_l, NS, n, 0, Sg, red);
+    blk_gram<R>(U_l, W_l, NS, n, 1, Ag, red);      // Ag = Uᵀmom and Sg = momᵀmom in one pass
     STAMP(6);
     const double tt = sq;
     const int nn = 2 * R;
@@ -266,7 +286,10 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
     for (int j = tid; j < n; j += kNT) {
       double x[2 * R];
 #pragma unroll
-      for (int l = 0; l < R; ++l) { x[l] = gptr(Ug)[j + (size_t)n * l]; x[R + l] = W_l[l * NS + j]; }
+      for (int l = 0; l < R; ++l) {
+        x[l] = L.keepU ? U_l[l * NS + j] : gptr(Ug)[j + (size_t)n * l];
+        x[R + l] = W_l[l * NS + j];
+      }
       double row1[R];
 #pragma unroll
       for (int l = 0; l < R; ++l) {
@@ -306,18 +329,11 @@ __global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
   }
 
   // ---- P5: temp[k,:,:] of the next step with the new U^(k) (phidotU, GPT_SGLD.jl:193-205)
-  const long long t1 = t + 1;
-  if (t1 < P.total_steps) {
-    const int e1 = (int)(t1 / P.nb), b1 = (int)(t1 - (long long)e1 * P.nb);
-    const int s1 = b1 * m;
-    const int B1 = min(m, P.N - s1);
-    const int32_t* ord1 = C.order + (size_t)e1 * P.N + s1;
-    __syncthreads();
-    for (int i = tid; i < B1; i += kNT) idx_l[i] = gptr(ord1)[i];
+  if (has_next) {
     __syncthreads();
     STAMP(9);
     double* tdst = C.temp + (size_t)(t1 & 1) * D * R * m + (size_t)k * R * m;
-    phidotU_tile<R>(C.phi, koff, rstride, idx_l, B1, n, NP, NS, U_l,
+    phidotU_tile<R>(C.phi, koff, rstride, ord1, 0, B1, n, NP, NS, U_l,
                     [&](int l, int i, double v) { gptr_w(tdst)[l * m + i] = v; });
     __syncthreads();
     STAMP(10);
@@ -343,7 +359,6 @@ __global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
   const int start = b * m;
   const int Bt = min(m, P.N - start);
   const int32_t* ord = C.order + (size_t)e * P.N + start;
-  for (int i = tid; i < Bt; i += kNT) idx_l[i] = ord[i];
   const double* Uk = C.U + (size_t)n * R * k;
   for (int o = tid; o < R * NP; o += kNT) {
     const int l = o / NP, j = o - l * NP;
@@ -351,7 +366,7 @@ __global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
   }
   __syncthreads();
   double* tdst = C.temp + (size_t)(t & 1) * D * R * m + (size_t)k * R * m;
-  phidotU_tile<R>(C.phi, (long long)n * k, (long long)n * D, idx_l, Bt, n, NP, NS, U_l,
+  phidotU_tile<R>(C.phi, (long long)n * k, (long long)n * D, ord, 0, Bt, n, NP, NS, U_l,
                   [&](int l, int i, double v) { tdst[l * m + i] = v; });
 }
 

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--n", type=int, default=500)
     ap.add_argument("--r", type=int, default=5)
     ap.add_argument("--m", type=int, default=50)
+    ap.add_argument("--sgd", action="store_true", help="langevin=False (no noise draws)")
+    ap.add_argument("--N", type=int, default=10000, help="training rows used (phi footprint)")
     args = ap.parse_args()
     import torch
     import bench
@@ -34,6 +36,7 @@ def main():
     dev = torch.device("cuda", 0)
     n, D, r, Q, m = args.n, 8, args.r, 200, args.m
     Xtr, ytr, _, _, _ = bench.kin40k(D)
+    Xtr, ytr = Xtr[:args.N], ytr[:args.N]
     ls = np.array([2.5242, 2.3376, 1.3630, 1.4949, 1.6022, 1.1366, 1.1964, 1.7028])
     I = G.samplenz(r, D, Q, 17)
     Z, b = G.feature_inputs(n, D, 17)
@@ -41,7 +44,7 @@ def main():
     phi = feature_device(tt(Xtr.T), tt(ls), 1.042, math.sqrt(n / Q ** (1 / D)), tt(Z.T), tt(b.T))
     y = tt(ytr)
     s = SGLDSession(phi, y, I, r, Q, m, 1e-5, 1e-8, 0.0476, 0, 3, list(range(1, args.chains + 1)),
-                    store=False)
+                    store=False, langevin=not args.sgd)
     s.run(50)
     s.sync()
     nb = (D + 1) * args.chains
