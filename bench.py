@@ -60,16 +60,18 @@ def cpu_baseline(phi_np, y_np, I, args, seconds):
     try:
         if ctx:
             ctx.__enter__()
-        kw = dict(store_every=10 ** 9)
-        steps = 5
+        N = phi_np.shape[2]
+        nb = -(-N // args.m)
+        steps, cap = 5, 20000
         while True:
+            epochs = -(-steps // nb)
             t0 = time.perf_counter()
             R.GPTregression(phi_np, y_np, args.signal_var, I, args.r, args.Q, args.m, args.epsw,
-                            args.epsU, 0, 1, 1, max_steps=steps, **kw)
+                            args.epsU, 0, epochs, 1, max_steps=steps, store_every=epochs * nb)
             dt = time.perf_counter() - t0
-            if dt >= seconds or steps >= 200:
+            if dt >= 0.8 * seconds or steps >= cap:
                 break
-            steps = min(200, max(steps + 1, int(steps * seconds / max(dt, 1e-3) * 1.05)))
+            steps = min(cap, max(steps + 1, int(steps * seconds / max(dt, 1e-3) * 1.05)))
     finally:
         if ctx:
             ctx.__exit__(None, None, None)
@@ -185,13 +187,12 @@ def main():
         pred_device(wp, Up, I0, phi_te, n, D, Nte, r, Q, 1, fh)
         fsum += fh
     torch.cuda.synchronize()
+    from gpt_amd.ensemble import combine_predictive_mean, rmse as ens_rmse
     ta = time.perf_counter()
-    if world > 1:
-        dist.all_reduce(fsum)                         # RCCL: predictive-mean gather (config 4)
-        torch.cuda.synchronize()
+    fmean = combine_predictive_mean(fsum, npred)     # RCCL all-reduce across ranks (config 4)
+    torch.cuda.synchronize()
     allreduce_ms = 1000.0 * (time.perf_counter() - ta)
-    fmean = (fsum / (npred * world)).cpu().numpy()
-    rmse = float(ysd * np.linalg.norm(yte - fmean) / math.sqrt(Nte))
+    rmse = ens_rmse(yte, fmean.cpu().numpy(), ysd)
 
     single = None
     if args.single_chain and rank == 0:

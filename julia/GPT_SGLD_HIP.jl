@@ -1,0 +1,153 @@
+# GPT_SGLD_HIP — drop-in replacement of the reference's `GPT_SGLD` module entry points on the
+# MI355X path, via `ccall` into libgptsgld.so (include/gptsgld.h).  Untested here (no Julia on the
+# image); mirrors the Python binding gpt_amd/GPT_SGLD.py, which is tested.
+#
+#   kin40kExperiment.jl:  `@everywhere using GPT_SGLD`  ->  `@everywhere using GPT_SGLD_HIP`
+#
+# Arrays are passed zero-copy (Julia column-major == the C ABI layout); outputs are allocated here,
+# exactly as the reference functions allocate and return them.
+module GPT_SGLD_HIP
+
+export datawhitening, feature, featureNotensor, samplenz, GPTregression, GPT_SGLDERM, pred, RMSE,
+       GPNT_SGLD
+
+const LIB = get(ENV, "GPTSGLD_LIB", joinpath(@__DIR__, "..", "gpt_amd", "libgptsgld.so"))
+
+struct SGLDConfig          # gpt_sgld_config
+    n::Int64; D::Int64; N::Int64; r::Int64; Q::Int64; m::Int64
+    epsw::Float64; epsU::Float64; signal_var::Float64; sigma_w::Float64
+    burnin::Int64; maxepoch::Int64; seed::UInt64
+    langevin::Int32; stiefel::Int32; store_every::Int64; max_steps::Int64
+end
+
+lasterr() = unsafe_string(ccall((:gpt_last_error, LIB), Cstring, ()))
+check(rc) = rc == 0 ? nothing : error("gptsgld error $rc: " * lasterr())
+
+# GPT_SGLD.jl:62-67 (host data prep, unchanged semantics)
+function datawhitening(X::Array)
+    X = copy(X)
+    for i = 1:size(X, 2)
+        X[:, i] = (X[:, i] .- sum(X[:, i]) / size(X, 1)) ./ sqrt(sum(abs2, X[:, i] .- sum(X[:, i]) / size(X, 1)) / (size(X, 1) - 1))
+    end
+    return X
+end
+
+# feature(X,length_scale,sigma_RBF,phi_scale,Z,b)  GPT_SGLD.jl:71
+function feature(X::Array{Float64,2}, length_scale, sigma_RBF::Real, phi_scale::Real,
+                 Z::Array{Float64,2}, b::Array{Float64})
+    N, D = size(X); n = size(Z, 1)
+    ls = collect(Float64, length_scale isa Real ? [length_scale] : length_scale)
+    phi = Array{Float64}(undef, n, D, N)
+    check(ccall((:gpt_feature, LIB), Cint,
+                (Ptr{Float64}, Int64, Int64, Ptr{Float64}, Int64, Float64, Float64, Ptr{Float64},
+                 Ptr{Float64}, Int64, Ptr{Float64}),
+                X, N, D, ls, length(ls), sigma_RBF, phi_scale, Z, b, n, phi))
+    return phi
+end
+
+# Generation-C seeded form used by kin40kExperiment.jl:71: feature(X,n,ls,σ,seed,scale)
+function feature(X::Array{Float64,2}, n::Integer, length_scale, sigma_RBF::Real, seed::Integer,
+                 scale::Real)
+    D = size(X, 2)
+    Z = Array{Float64}(undef, n, D); b = Array{Float64}(undef, n, D)
+    check(ccall((:gpt_feature_inputs, LIB), Cint, (Int64, Int64, UInt64, Ptr{Float64}, Ptr{Float64}),
+                n, D, seed, Z, b))
+    return feature(X, length_scale, sigma_RBF, scale, Z, b)
+end
+
+# featureNotensor(X,length_scale,sigma_RBF,Z,b)  GPT_SGLD.jl:109
+function featureNotensor(X::Array{Float64,2}, length_scale, sigma_RBF::Real, Z::Array{Float64,2},
+                         b::Array{Float64})
+    N, D = size(X); n = size(Z, 1)
+    ls = collect(Float64, length_scale isa Real ? [length_scale] : length_scale)
+    phi = Array{Float64}(undef, n, N)
+    check(ccall((:gpt_feature_notensor, LIB), Cint,
+                (Ptr{Float64}, Int64, Int64, Ptr{Float64}, Int64, Float64, Ptr{Float64},
+                 Ptr{Float64}, Int64, Ptr{Float64}),
+                X, N, D, ls, length(ls), sigma_RBF, Z, b, n, phi))
+    return phi
+end
+
+# samplenz(r,D,Q,seed)  GPT_SGLD_p.jl:57
+function samplenz(r::Integer, D::Integer, Q::Integer, seed::Integer=0)
+    I = Array{Int32}(undef, Q, D)
+    check(ccall((:gpt_samplenz, LIB), Cint, (Int64, Int64, Int64, UInt64, Ptr{Int32}), r, D, Q, seed, I))
+    return I
+end
+
+# GPTregression(phi,y,signal_var,I,r,Q,m,epsw,epsU,burnin,maxepoch,param_seed;langevin,stiefel)
+# GPT_SGLD.jl:345 — returns (w_store, U_store); NaN in the geodesic -> message + zeros (:422-424).
+function GPTregression(phi::Array{Float64,3}, y::Array{Float64}, signal_var::Real, I::Array{Int32,2},
+                       r::Integer, Q::Integer, m::Integer, epsw::Real, epsU::Real, burnin::Integer,
+                       maxepoch::Integer, param_seed::Integer=0; langevin=true, stiefel=true,
+                       sigma_w::Real=1.0, store_every::Integer=1)
+    n, D, N = size(phi)
+    numbatches = cld(N, m)
+    T = div(maxepoch * numbatches, store_every)
+    cfg = Ref(SGLDConfig(n, D, N, r, Q, m, epsw, epsU, signal_var, sigma_w, burnin, maxepoch,
+                         UInt64(param_seed), Int32(langevin), Int32(stiefel), store_every, 0))
+    w_store = zeros(Q, T); U_store = zeros(n, r, D, T)
+    rc = ccall((:gpt_sgld_regression, LIB), Cint,
+               (Ref{SGLDConfig}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64},
+                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+               cfg, phi, vec(y), I, C_NULL, C_NULL, w_store, U_store, C_NULL)
+    if rc == 1
+        println("Get NaN when moving along Geodesic. Try smaller epsU")
+        return zeros(Q, T), zeros(n, r, D, T)
+    end
+    check(rc)
+    return w_store, U_store
+end
+
+# GPT_SGLDERM(phi,y,sigma,I,r,Q,m,epsw,epsU,burnin,maxepoch)  GPT_SGLD_p.jl:146 (σ_w=√(nᴰ/Q))
+function GPT_SGLDERM(phi::Array{Float64,3}, y::Array{Float64}, sigma::Real, I::Array{Int32,2},
+                     r::Integer, Q::Integer, m::Integer, epsw::Real, epsU::Real, burnin::Integer,
+                     maxepoch::Integer, param_seed::Integer=0)
+    n, D, _ = size(phi)
+    return GPTregression(phi, y, sigma^2, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed;
+                         sigma_w=sqrt(Float64(n)^D / Q))
+end
+
+# pred(w,U,I,phitest)  GPT_SGLD.jl:233
+function pred(w::Array{Float64}, U::Array{Float64,3}, I::Array{Int32,2}, phitest::Array{Float64,3})
+    n, D, Nt = size(phitest); r = size(U, 2); Q = length(w)
+    f = Array{Float64}(undef, Nt)
+    check(ccall((:gpt_pred, LIB), Cint,
+                (Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Int64, Int64, Int64, Int64, Int64,
+                 Ptr{Float64}), vec(w), U, I, phitest, n, D, Nt, r, Q, f))
+    return f
+end
+
+# RMSE(w_store,U_store,I,phitest,ytest)  GPT_SGLD_p.jl:124 — mean prediction over all samples
+function RMSE(w_store::Array{Float64,2}, U_store::Array{Float64,4}, I::Array{Int32,2},
+              phitest::Array{Float64,3}, ytest::Array{Float64})
+    n, D, Nt = size(phitest); r = size(U_store, 2); Q, S = size(w_store)
+    meanf = Array{Float64}(undef, Nt); out = Ref(0.0)
+    check(ccall((:gpt_pred_mean, LIB), Cint,
+                (Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64}, Int64, Int64, Int64,
+                 Int64, Int64, Int64, Float64, Ptr{Float64}, Ref{Float64}),
+                w_store, U_store, I, phitest, vec(ytest), n, D, Nt, r, Q, S, 1.0, meanf, out))
+    return out[]
+end
+
+# GPNT_SGLD(phi,y,signal_var,sigma_theta,m,eps_theta,decay_rate,burnin,maxepoch,param_seed)
+# GPT_SGLD.jl:809
+function GPNT_SGLD(phi::Array{Float64,2}, y::Array{Float64}, signal_var::Real, sigma_theta::Real,
+                   m::Integer, eps_theta::Real, decay_rate::Real, burnin::Integer, maxepoch::Integer,
+                   param_seed::Integer)
+    n, N = size(phi)
+    store = Array{Float64}(undef, n, (maxepoch + burnin) * cld(N, m))
+    rc = ccall((:gpt_gpnt_sgld, LIB), Cint,
+               (Ptr{Float64}, Ptr{Float64}, Int64, Int64, Float64, Float64, Int64, Float64, Float64,
+                Int64, Int64, UInt64, Ptr{Float64}),
+               phi, vec(y), n, N, signal_var, sigma_theta, m, eps_theta, decay_rate, burnin, maxepoch,
+               param_seed, store)
+    if rc == 4
+        println("Get NaN in theta. Try smaller epsilon")
+        return zeros(n)
+    end
+    check(rc)
+    return store
+end
+
+end # module
