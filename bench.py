@@ -86,7 +86,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--chains", type=int, default=28, help="independent chains per GPU")
+    ap.add_argument("--chains", type=int, default=0,
+                    help="independent chains per GPU (0: one per CU for the chain engine, "
+                         "28 (x D+1 workgroups) for the grid engine)")
+    ap.add_argument("--engine", default="auto", choices=["auto", "grid", "chain"])
     ap.add_argument("--n", type=int, default=500)
     ap.add_argument("--D", type=int, default=8)
     ap.add_argument("--r", type=int, default=5)
@@ -134,11 +137,18 @@ def main():
 
     nb = -(-N // m)
     C = args.chains
+    if C <= 0:
+        probe = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0, 1,
+                            [1], store=False, engine=args.engine)
+        eng = probe.info()["engine"]
+        probe.close()
+        C = torch.cuda.get_device_properties(dev).multi_processor_count if eng == "chain" else 28
     need = args.warmup + args.steps + args.kernel_steps
     epochs = -(-need // nb) + 1
     seeds = [1000 * rank + c + 1 for c in range(C)]
     sess = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0, epochs,
-                       seeds, store_every=nb, store=True)
+                       seeds, store_every=nb, store=True, engine=args.engine)
+    info = sess.info()
     sess.run(args.warmup)
     sess.sync()
     if world > 1:
@@ -197,7 +207,7 @@ def main():
     single = None
     if args.single_chain and rank == 0:
         s1 = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0,
-                         epochs, [7], store_every=nb, store=False)
+                         epochs, [7], store_every=nb, store=False, engine=args.engine)
         s1.run(args.warmup); s1.sync()
         t1 = time.perf_counter(); s1.run(args.steps); s1.sync()
         single = args.steps / (time.perf_counter() - t1)
@@ -225,10 +235,13 @@ def main():
             "config": {"workload": "kin40k tensor-GP SGLD (GPTregression)", "Ntrain": N, "Ntest": Nte,
                        "D": D, "n_features": n, "r": r, "Q": Q, "minibatch": m,
                        "chains_per_gpu": C, "epsw": args.epsw, "epsU": args.epsU,
-                       "signal_var": args.signal_var, "parallelism": "chains%dx%d" % (C, world)},
+                       "signal_var": args.signal_var, "parallelism": "chains%dx%d" % (C, world),
+                       "engine": info["engine"], "workgroups_per_launch": info["workgroups"],
+                       "threads_per_workgroup": info["threads"], "lds_bytes": info["lds_bytes"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "sgld_step_kernel<5>", "kernel_us": k_us,
+                         "kernel": ("chain_kernel<%d,J,2>" if info["engine"] == "chain"
+                                    else "sgld_step_kernel<%d>") % r, "kernel_us": k_us,
                          "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "test_rmse": rmse,

@@ -26,7 +26,9 @@ Arrays follow Julia's column-major layout: ``phi`` is (n, D, N) Fortran-ordered,
 RNG: Julia's MersenneTwister stream is replaced by the framework's Philox contract
 (oracle/philox.py documents it); seeds play the same role (``srand(param_seed)``).
 """
+import contextlib
 import math
+import os
 
 import numpy as np
 
@@ -150,11 +152,32 @@ def init_state(n, r, D, Q, seed, stiefel=True, sigma_w=1.0):
     return w, U
 
 
+@contextlib.contextmanager
+def _engine_env(engine):
+    """GPTSGLD_ENGINE for the duration of one host-API call (the library reads it at session
+    creation; include/gptsgld.h gpt_sgld_session_info)."""
+    if engine is None:
+        yield
+        return
+    if engine not in ("grid", "chain", "auto"):
+        raise ValueError("engine must be 'grid', 'chain' or 'auto'")
+    old = os.environ.get("GPTSGLD_ENGINE")
+    os.environ["GPTSGLD_ENGINE"] = engine
+    try:
+        yield
+    finally:
+        if old is None:
+            del os.environ["GPTSGLD_ENGINE"]
+        else:
+            os.environ["GPTSGLD_ENGINE"] = old
+
+
 def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0,
                   langevin=True, stiefel=True, sigma_w=1.0, store_every=1, max_steps=0,
-                  w_init=None, U_init=None, diag=False):
+                  w_init=None, U_init=None, diag=False, engine=None):
     """Tensor-GP regression sampler (GPT_SGLD.jl:345-448).  Returns (w_store, U_store)
-    [, diag]; ``diag`` = per-step [‖gradw‖, ‖gradU_1‖, …] ((1+D) × steps)."""
+    [, diag]; ``diag`` = per-step [‖gradw‖, ‖gradU_1‖, …] ((1+D) × steps).
+    ``engine`` ("grid" | "chain" | None = library default) selects the step kernel."""
     phi = _f64(phi)
     n, D, N = phi.shape
     y = _f64(np.asarray(y, dtype=np.float64).ravel())
@@ -173,10 +196,11 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
     dg = np.zeros((1 + D, total), order="F") if diag else None
     wi = _f64(w_init) if w_init is not None else None
     Ui = _f64(U_init) if U_init is not None else None
-    code = lib().gpt_sgld_regression(C.byref(cfg), _ptr(phi), _ptr(y), _ptr(I, P_I32),
-                                     _ptr(wi) if wi is not None else None,
-                                     _ptr(Ui) if Ui is not None else None,
-                                     _ptr(w_store), _ptr(U_store), _ptr(dg) if diag else None)
+    with _engine_env(engine):
+        code = lib().gpt_sgld_regression(C.byref(cfg), _ptr(phi), _ptr(y), _ptr(I, P_I32),
+                                         _ptr(wi) if wi is not None else None,
+                                         _ptr(Ui) if Ui is not None else None,
+                                         _ptr(w_store), _ptr(U_store), _ptr(dg) if diag else None)
     if code == _lib.GPT_ERR_NAN_GEODESIC:
         print("Get NaN when moving along Geodesic. Try smaller epsU")
         w_store[:] = 0.0

@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgptsgld.so")
+LIB_PATH = os.environ.get("GPTSGLD_LIB") or os.path.join(_HERE, "libgptsgld.so")
 
 GPT_OK = 0
 GPT_ERR_NAN_GEODESIC = 1
@@ -58,6 +58,7 @@ SIGNATURES = {
                                   C.c_void_p, C.c_void_p]),
     "gpt_sgld_session_fetch": (C.c_int, [C.c_void_p, C.c_int32, P_D, P_D, P_D, P_I32]),
     "gpt_sgld_session_destroy": (None, [C.c_void_p]),
+    "gpt_sgld_session_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
     "gpt_pred": (C.c_int, [P_D, P_D, P_I32, P_D, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                            C.c_int64, P_D]),
     "gpt_pred_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,

@@ -7,6 +7,7 @@
 // reference does the same draws on the CPU, GPT_SGLD.jl:357-373), moves buffers and launches.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -164,7 +165,9 @@ static bool valid_cfg(const gpt_sgld_config* c) {
   if (c->store_every < 1) { set_error("store_every must be >= 1"); return false; }
   if (!(c->signal_var > 0) || !(c->sigma_w > 0)) { set_error("variances must be > 0"); return false; }
   const StepLayout L = step_layout((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m);
-  if (L.bytes > 160 * 1024) {
+  const bool chain_ok = chain_supported((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m,
+                                        c->langevin != 0, c->stiefel != 0);
+  if (L.bytes > 160 * 1024 && !chain_ok) {
     set_error("working set exceeds 160 KiB LDS (n*r, Q*D or m too large)"); return false;
   }
   return true;
@@ -191,7 +194,55 @@ struct gpt_sgld_session {
   hipGraphExec_t gexec = nullptr;
   int graph_steps = 0;
   bool store = false, diag = false;
+  int engine = 0;                     // kEngineGrid / kEngineChain
+  DevMem segpos;
 };
+
+// Engine choice: store_flags bit 2 forces the grid engine (sgld.hip), bit 3 the chain engine
+// (chain.hip); otherwise GPTSGLD_ENGINE=grid|chain, otherwise chain whenever it supports the shape.
+static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t flags,
+                       int* engine) {
+  int max_run = 0;                    // longest run of core entries sharing one I[·,k] value
+  for (int k = 0; k < (int)c->D; ++k) {
+    std::vector<int> cnt((size_t)c->r + 1, 0);
+    for (int q = 0; q < (int)c->Q; ++q) max_run = std::max(max_run, ++cnt[I_host[q + c->Q * k]]);
+  }
+  const bool chain_ok = chain_supported((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m,
+                                        c->langevin != 0, c->stiefel != 0, max_run);
+  const bool grid_ok =
+      step_layout((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m).bytes <= 160 * 1024;
+  int want = -1;
+  if (flags & 4) want = kEngineGrid;
+  else if (flags & 8) want = kEngineChain;
+  else if (const char* ev = std::getenv("GPTSGLD_ENGINE")) {
+    if (!std::strcmp(ev, "grid")) want = kEngineGrid;
+    else if (!std::strcmp(ev, "chain")) want = kEngineChain;
+  }
+  if (want == kEngineChain && !chain_ok) {
+    set_error("chain engine does not support this shape (needs D<=8, r<=5, n<=512 (even if >64), "
+              "Q<=256, SGLD+Stiefel, <=64 core entries per I[.,k] value)");
+    return GPT_ERR_BAD_DIMS;
+  }
+  if (want == kEngineGrid && !grid_ok) {
+    set_error("grid engine: working set exceeds 160 KiB LDS"); return GPT_ERR_BAD_DIMS;
+  }
+  *engine = want >= 0 ? want : (chain_ok ? kEngineChain : kEngineGrid);
+  return GPT_OK;
+}
+
+// Chain engine tables: for every dimension k the core entries ordered by (I[q,k], q):
+// pos[q + Q*k] = rank of q, seg[k*(r+1) + l] = first rank with I[q,k] = l (0-based).
+static void chain_segpos(const std::vector<int32_t>& I0, int Q, int D, int r,
+                         std::vector<int32_t>& out) {
+  out.assign((size_t)Q * D + (size_t)D * (r + 1), 0);
+  for (int k = 0; k < D; ++k) {
+    std::vector<int> cnt(r + 1, 0);
+    for (int q = 0; q < Q; ++q) cnt[I0[q + (size_t)Q * k] + 1]++;
+    for (int l = 0; l < r; ++l) cnt[l + 1] += cnt[l];
+    for (int l = 0; l <= r; ++l) out[(size_t)Q * D + (size_t)k * (r + 1) + l] = cnt[l];
+    for (int q = 0; q < Q; ++q) out[q + (size_t)Q * k] = cnt[I0[q + (size_t)Q * k]]++;
+  }
+}
 
 extern "C" const char* gpt_last_error(void) { return g_err.c_str(); }
 
@@ -205,10 +256,27 @@ extern "C" int gpt_device_count(void) {
   return c;
 }
 
+static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t_local) {
+  if (s->engine == kEngineChain)
+    return launch_chain(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
+                        t_local, s->stream);
+  return launch_step(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
+                     t_local, s->stream);
+}
+
+// temp of the first step (grid engine only: the chain engine forms temp inside its step).
+static int session_prime(gpt_sgld_session* s) {
+  if (s->engine != kEngineGrid || s->temp_ready) return GPT_OK;
+  hipError_t e = launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
+                                  s->tbase.as<long long>(), s->stream);
+  if (e != hipSuccess) return hip_fail(e, "launch_temp_init");
+  s->temp_ready = true;
+  return GPT_OK;
+}
+
 static int session_enqueue(gpt_sgld_session* s, int count) {
   for (int i = 0; i < count; ++i) {
-    hipError_t e = launch_step(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
-                               s->tbase.as<long long>(), i, s->stream);
+    hipError_t e = session_launch(s, s->P, i);
     if (e != hipSuccess) return hip_fail(e, "launch_step");
   }
   hipError_t e = launch_advance(s->tbase.as<long long>(), count, s->stream);
@@ -235,6 +303,10 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   if (he != hipSuccess) return hip_fail(he, "hipFuncSetAttribute");
 
   std::unique_ptr<gpt_sgld_session> s(new gpt_sgld_session());
+  {
+    const int rc = pick_engine(cfg, I_host, store_flags, &s->engine);
+    if (rc != GPT_OK) return rc;
+  }
   s->cfg = *cfg;
   s->nchains = nchains;
   s->numbatches = (N + m - 1) / m;
@@ -261,6 +333,14 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   HIPCHK(s->I0.alloc(sizeof(int32_t) * I0.size()));
   HIPCHK(hipMemcpy(s->I0.p, I0.data(), sizeof(int32_t) * I0.size(), hipMemcpyHostToDevice));
   P.I0 = s->I0.as<int32_t>();
+  P.segpos = nullptr;
+  if (s->engine == kEngineChain) {
+    std::vector<int32_t> sp;
+    chain_segpos(I0, Q, D, r, sp);
+    HIPCHK(s->segpos.alloc(sizeof(int32_t) * sp.size()));
+    HIPCHK(hipMemcpy(s->segpos.p, sp.data(), sizeof(int32_t) * sp.size(), hipMemcpyHostToDevice));
+    P.segpos = s->segpos.as<int32_t>();
+  }
   P.stamps = nullptr;
   HIPCHK(s->tbase.alloc(sizeof(long long)));
   HIPCHK(hipMemset(s->tbase.p, 0, sizeof(long long)));
@@ -335,11 +415,9 @@ extern "C" int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps) {
   if (!s) { set_error("null session"); return GPT_ERR_BAD_DIMS; }
   long long remaining = std::min<long long>(nsteps, s->total_steps - s->steps_done);
   if (remaining <= 0) return GPT_OK;
-  if (!s->temp_ready) {
-    hipError_t e = launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
-                                    s->tbase.as<long long>(), s->stream);
-    if (e != hipSuccess) return hip_fail(e, "launch_temp_init");
-    s->temp_ready = true;
+  {
+    const int rc = session_prime(s);
+    if (rc != GPT_OK) return rc;
   }
   while (remaining > 0) {
     const int chunk = (int)std::min<long long>(remaining, s->graph_steps);
@@ -370,19 +448,16 @@ extern "C" int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, 
   const long long cnt = std::min<long long>(nsteps, s->total_steps - s->steps_done);
   if (avg_us) *avg_us = 0.0;
   if (cnt <= 0) return GPT_OK;
-  if (!s->temp_ready) {
-    hipError_t e = launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
-                                    s->tbase.as<long long>(), s->stream);
-    if (e != hipSuccess) return hip_fail(e, "launch_temp_init");
-    s->temp_ready = true;
+  {
+    const int rc = session_prime(s);
+    if (rc != GPT_OK) return rc;
   }
   std::vector<hipEvent_t> ev(2 * cnt, nullptr);
   for (auto& e : ev) HIPCHK(hipEventCreate(&e));
   int rc = GPT_OK;
   for (long long i = 0; i < cnt && rc == GPT_OK; ++i) {
     HIPCHK(hipEventRecord(ev[2 * i], s->stream));
-    hipError_t e = launch_step(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
-                               s->tbase.as<long long>(), (int)i, s->stream);
+    hipError_t e = session_launch(s, s->P, (int)i);
     if (e != hipSuccess) rc = hip_fail(e, "launch_step");
     HIPCHK(hipEventRecord(ev[2 * i + 1], s->stream));
   }
@@ -408,11 +483,9 @@ extern "C" int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int6
   if (!s || !out) { set_error("null argument"); return GPT_ERR_BAD_DIMS; }
   const long long cnt = std::min<long long>(nsteps, s->total_steps - s->steps_done);
   if (cnt <= 0) return GPT_OK;
-  if (!s->temp_ready) {
-    hipError_t e = launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
-                                    s->tbase.as<long long>(), s->stream);
-    if (e != hipSuccess) return hip_fail(e, "launch_temp_init");
-    s->temp_ready = true;
+  {
+    const int rc = session_prime(s);
+    if (rc != GPT_OK) return rc;
   }
   const size_t per = (size_t)(s->P.D + 1) * s->nchains * kStamps;
   DevMem buf;
@@ -421,8 +494,7 @@ extern "C" int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int6
   StepParams P = s->P;
   for (long long i = 0; i < cnt; ++i) {
     P.stamps = buf.as<long long>() + per * i;
-    hipError_t e = launch_step(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
-                               (int)i, s->stream);
+    hipError_t e = session_launch(s, P, (int)i);
     if (e != hipSuccess) return hip_fail(e, "launch_step");
   }
   hipError_t e = launch_advance(s->tbase.as<long long>(), cnt, s->stream);
@@ -430,6 +502,22 @@ extern "C" int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int6
   HIPCHK(hipStreamSynchronize(s->stream));
   HIPCHK(hipMemcpy(out, buf.p, 8 * per * cnt, hipMemcpyDeviceToHost));
   s->steps_done += cnt;
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_info(gpt_sgld_session* s, int64_t* out) {
+  if (!s || !out) { set_error("null argument"); return GPT_ERR_BAD_DIMS; }
+  const StepParams& P = s->P;
+  out[0] = s->engine;
+  if (s->engine == kEngineChain) {
+    out[1] = (int64_t)chain_lds_bytes(P.n, P.D, P.r, P.Q, P.m);
+    out[2] = 64 * P.D;
+    out[3] = s->nchains;
+  } else {
+    out[1] = (int64_t)step_layout(P.n, P.D, P.r, P.Q, P.m).bytes;
+    out[2] = kNT;
+    out[3] = (int64_t)(P.D + 1) * s->nchains;
+  }
   return GPT_OK;
 }
 

@@ -1,0 +1,646 @@
+// Chain-resident SGLD engine for MI355X (gfx950): one workgroup per chain.
+//
+// Workgroup = D waves; wave k owns U^(k) (n×r) in REGISTERS for the step (lane λ holds rows
+// j = λ + 64·jj, jj < J).  A step (GPT_SGLD.jl:377-445) streams its minibatch G rows at a time;
+// each row slice phi[:,k,row] is read from HBM ONCE — staged into this wave's LDS slice by
+// LDS-DMA (global_load_lds) one group ahead — and used twice from registers:
+//   (b) temp[k,:,row]  = phi[:,k,row]ᵀ U^(k)                    (phidotU, :193-205)
+//   (c) V, fhat and the core sums A[:,k,row] for the G rows, all waves together
+//       (computeV / computefhat / computeU_phi / computeA, :208-273)
+//   (e) gradU^(k) += phi[:,k,row] · (A[:,k,row]·res_row)ᵀ        (computePsi + Psi·res, :276-408)
+// The grid engine (sgld.hip) reads the batch twice.  After the batch: the w update (block-wide)
+// and, per wave with no block barrier, the Langevin drive, Stiefel projection, geodesic (two Padé
+// expm on the wave) and renormalisation of U^(k) in registers.
+//
+// The A sums are segmented: for every k the core entries q are ordered by (I[q,k], q) on the host
+// (segpos), so A[l,k,row] is a contiguous run of w_q·V_q/temp[k,I[q,k],row] — fixed order, no
+// atomics.  1/temp is formed once per (k, l, row) when temp is, so the Q·D divisions of
+// computeU_phi become multiplications.
+#include "device_util.h"
+
+namespace gpt {
+
+#ifndef CHAIN_STAGE_AT
+#define CHAIN_STAGE_AT 2          // where the next group's rows are staged: 0 (a), 1 (c), 2 (e)
+#endif
+constexpr int kChainDMax = 8;     // waves per workgroup (one per input dimension)
+constexpr int kChainTasks = 2;    // V-phase tasks per wave (NCH·G <= tasks·D); J = 8: 1
+constexpr int kChainG = 2;        // batch rows per group
+constexpr int kChainQPL = 4;      // q chunks of 64 (Q <= 64·kChainQPL)
+constexpr int kChainQP = 64 * kChainQPL;
+constexpr int kChainRun = 64;     // slots per run (core entries with one value of I[·,k]) per row
+
+struct ChainLayout {
+  int NCH, NT;                    // q chunks of 64, tasks = NCH·G
+  int TS;                         // doubles per temp slot: temp | ones(G) | 1/temp | ones(G)
+  size_t o_IT, o_pos, o_w, o_idx, o_y, o_temp, o_fp, o_gwp, o_misc, o_un, bytes;
+  size_t L_dbl, x_dbl;            // union tenants (doubles): run buffer | per-wave scratch
+};
+
+// Per-wave scratch after the batch: S0 = max(expm<2r> scratch, noise slots) | E[:,1:r] | grams.
+GPT_HD size_t chain_scratch_dbl(int r) {
+  const size_t s0a = 7 * 4 * (size_t)r * r, s0b = 64 * (size_t)(r + (r & 1));
+  return (s0a > s0b ? s0a : s0b) + 2 * (size_t)r * r + 3 * (size_t)r * r + r;
+}
+
+GPT_HD ChainLayout chain_layout(int n, int D, int r, int Q, int m, int G) {
+  (void)n;
+  ChainLayout L;
+  L.NCH = (Q + 63) / 64;
+  L.NT = L.NCH * G;
+  L.TS = 2 * (D * r * G + G);
+  size_t o = 0;
+  // index tables for all kChainDMax dimensions (rows k >= D point at the ones / trash slots)
+  L.o_IT = o;   o = al16(o + 4 * (size_t)Q * kChainDMax);
+  L.o_pos = o;  o = al16(o + 4 * (size_t)Q * kChainDMax);
+  L.o_w = o;    o = al16(o + 8 * (size_t)Q);
+  L.o_idx = o;  o = al16(o + 4 * (size_t)m);
+  L.o_y = o;    o = al16(o + 8 * (size_t)m);
+  L.o_temp = o; o = al16(o + 8 * 2 * (size_t)L.TS);           // 2 slots
+  L.o_fp = o;   o = al16(o + 8 * (size_t)kChainQPL * G);
+  L.o_gwp = o;  o = al16(o + 8 * (size_t)L.NT * 64);
+  L.o_misc = o; o = al16(o + 8 * 16);
+  L.o_un = o;
+  L.L_dbl = (size_t)kChainDMax * G * r * kChainRun;            // runs: [k][row][l][slot]
+  L.x_dbl = chain_scratch_dbl(r);
+  const size_t un = 8 * (L.L_dbl > L.x_dbl * D ? L.L_dbl : L.x_dbl * D);
+  L.bytes = al16(o + un);
+  return L;
+}
+
+// Diagnostic phase stamps (gpt_sgld_session_stamps only): s_memtime of wave 0 at phase ends.
+#define CSTAMP(slot)                                                                        \
+  do {                                                                                      \
+    if (P.stamps && tid == 0)                                                               \
+      P.stamps[(size_t)blockIdx.x * kStamps + (slot)] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+// Workgroup barrier that orders LDS only: an LDS-DMA prefetch stays in flight across it
+// (__syncthreads() would also drain vmcnt).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Wave-wide sums of NV per-lane values written to dst[0..NV) (and, with dst2, values NV..2NV-1
+// to dst2[0..NV)); the caller orders the LDS writes with wave_sync().
+template <int NV>
+__device__ __forceinline__ void wave_sum_to_lds(double (&v)[NV], double* dst) {
+  constexpr int NB = NV <= 8 ? 8 : (NV <= 16 ? 16 : (NV <= 32 ? 32 : 64));
+  const int lane = threadIdx.x & 63;
+  double b[NB];
+#pragma unroll
+  for (int x = 0; x < NB; ++x) b[x] = x < NV ? v[x] : 0.0;
+  Butterfly<NB>::run(b, lane);
+  constexpr int SH = 6 - Butterfly<NB>::P;
+  const int vi = lane >> SH;
+  if ((lane & ((1 << SH) - 1)) == 0 && vi < NV) dst[vi] = b[0];
+}
+template <int NV>
+__device__ __forceinline__ void wave_sum_to_lds(double (&v)[2 * NV], double* dst, double* dst2) {
+  constexpr int NB = 2 * NV <= 8 ? 8 : (2 * NV <= 16 ? 16 : (2 * NV <= 32 ? 32 : 64));
+  const int lane = threadIdx.x & 63;
+  double b[NB];
+#pragma unroll
+  for (int x = 0; x < NB; ++x) b[x] = x < 2 * NV ? v[x] : 0.0;
+  Butterfly<NB>::run(b, lane);
+  constexpr int SH = 6 - Butterfly<NB>::P;
+  const int vi = lane >> SH;
+  if ((lane & ((1 << SH) - 1)) == 0 && vi < 2 * NV) {
+    if (vi < NV) dst[vi] = b[0];
+    else dst2[vi - NV] = b[0];
+  }
+}
+
+template <int R, int J, int G>
+__global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
+                                                                const ChainDesc* chains,
+                                                                const long long* __restrict__ tbase,
+                                                                int t_local) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ __attribute__((aligned(16))) double pbuf[kChainDMax * G * 64 * J];   // row staging
+  // Chain fields are read through Cp at their point of use (scalar loads) rather than held in
+  // SGPRs across the batch loop, where SGPR pressure spills into VGPR lanes.
+  const ChainDesc* Cp = chains + blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, k = uni(tid >> 6);
+  const int n = P.n, D = P.D, Q = P.Q, m = P.m, NTH = 64 * D;
+  const ChainLayout L = chain_layout(n, D, R, Q, m, G);
+  int* IT_l = (int*)(smem + L.o_IT);
+  int* pos_l = (int*)(smem + L.o_pos);
+  double* w_l = (double*)(smem + L.o_w);
+  int* idx_l = (int*)(smem + L.o_idx);
+  double* y_l = (double*)(smem + L.o_y);
+  double* temp_l = (double*)(smem + L.o_temp);
+  double* fp_l = (double*)(smem + L.o_fp);
+  double* gwp_l = (double*)(smem + L.o_gwp);
+  double* misc = (double*)(smem + L.o_misc);
+  int* flag = (int*)(misc + 8);
+  double* Lseg = (double*)(smem + L.o_un);
+  double* X = (double*)(smem + L.o_un) + (size_t)k * L.x_dbl;   // this wave's scratch
+  double* xi_l = X;                                             // noise slots (before expm)
+  double* pw = pbuf + k * (G * 64 * J);                         // this wave's staged rows
+
+  const long long t = tbase[0] + t_local;
+  if (t >= P.total_steps) return;
+  if (__hip_atomic_load(Cp->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  CSTAMP(0);
+
+  // ---- prologue: index tables, w, batch rows, and U^(k) into registers
+  const int DRG = D * R * G;
+  {
+    // IT_l[kk·Q+q]: temp index (kk·R + I[q,kk])·G of the core entry (+gg at use); rows kk >= D
+    // point at the ones slot.  pos_l: run slot ((kk·G)·R + l)·64 + (rank of q within run l)
+    // (+gg·R·64 at use), l = I[q,kk]; rows kk >= D land in never-read trash rows.
+    const int32_t* segp = P.segpos + (size_t)Q * D;
+    for (int o = tid; o < Q * kChainDMax; o += NTH) {
+      const int kk = o / Q, q = o - kk * Q;
+      if (kk < D) {
+        const int l = gptr(P.I0)[q + Q * kk];
+        IT_l[o] = (kk * R + l) * G;
+        pos_l[o] = (kk * G * R + l) * kChainRun +
+                   (gptr(P.segpos)[q + Q * kk] - gptr(segp)[kk * (R + 1) + l]);
+      } else {
+        IT_l[o] = DRG;
+        pos_l[o] = kk * G * R * kChainRun;
+      }
+    }
+    for (int o = tid; o < D * G * R * kChainRun; o += NTH) Lseg[o] = 0.0;   // empty slots read 0
+    for (int o = tid; o < 2 * G; o += NTH) {                     // ones slots of both temp slots
+      temp_l[o / G * L.TS + DRG + o % G] = 1.0;
+      temp_l[o / G * L.TS + 2 * DRG + G + o % G] = 1.0;
+    }
+    for (int o = tid; o < kChainQPL * G; o += NTH) fp_l[o] = 0.0;
+  }
+  for (int q = tid; q < Q; q += NTH) w_l[q] = gptr(Cp->w)[(size_t)(t & 1) * Q + q];
+  if (tid == 0) flag[0] = 0;
+  const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
+  const int start = b * m;
+  const int Bt = min(m, P.N - start);
+  {
+    const int32_t* ord = Cp->order + (size_t)e * P.N + start;
+    const double* yv = Cp->y;
+    for (int i = tid; i < Bt; i += NTH) {
+      const int row = gptr(ord)[i];
+      idx_l[i] = row;
+      y_l[i] = gptr(yv)[row];
+    }
+  }
+  double u[J][R];
+  {
+    const double* Ug = Cp->U + (size_t)n * R * k;
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = lane + 64 * jj;
+      const int jc = min(j, n - 1);          // unconditional in-bounds loads, padding rows zeroed
+#pragma unroll
+      for (int l = 0; l < R; ++l) {
+        const double x = gptr(Ug + (size_t)n * l)[jc];
+        u[jj][l] = j < n ? x : 0.0;
+      }
+    }
+  }
+  __syncthreads();
+  CSTAMP(1);
+
+  const long long koff = (long long)n * k, rstride = (long long)n * D;
+  const double* phi_k = uni_ptr(Cp->phi) + koff;
+  // Stage rows g0n .. g0n+G-1 of this wave's dimension into pw (lane-linear LDS image: double j
+  // of row gg at pw[gg·64J + j]); bytes past the row end are clamped in-row and never read.
+  auto stage = [&](int g0n, int ln) {
+    int rows[G];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) rows[gg] = uni(idx_l[min(g0n + gg, Bt - 1)]);
+    // no LDS read between the DMA issues below: a DS read after a pending LDS-DMA may be
+    // ordered behind it (vmcnt) by the compiler
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      const char* rb = (const char*)(phi_k + (long long)rows[gg] * rstride);
+      __attribute__((address_space(3))) double* dst =
+          (__attribute__((address_space(3))) double*)(pw + gg * 64 * J);
+      if constexpr (J >= 2) {           // n even (chain_supported): 16-B pieces, J/2 per row
+#pragma unroll
+        for (int s = 0; s < J / 2; ++s) {
+          const unsigned o = min(16u * ln + 1024u * s, 8u * n - 16u);
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(rb + o),
+                                           (__attribute__((address_space(3))) void*)(dst + 128 * s),
+                                           16, 0, 0);
+        }
+      } else {                          // n <= 64: 4-B pieces, 2 per row
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const unsigned o = min(4u * ln + 256u * s, 8u * n - 4u);
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(rb + o),
+                                           (__attribute__((address_space(3))) void*)(dst + 32 * s),
+                                           4, 0, 0);
+        }
+      }
+    }
+  };
+  stage(0, lane);
+
+  constexpr int NVB = R <= 8 ? 8 : (R <= 16 ? 16 : (R <= 32 ? 32 : 64));
+  constexpr int SHB = 6 - Butterfly<NVB>::P;
+
+  double acc[J][R];
+#pragma unroll
+  for (int jj = 0; jj < J; ++jj)
+#pragma unroll
+    for (int l = 0; l < R; ++l) acc[jj][l] = 0.0;
+  constexpr int TPW = J >= 8 ? 1 : kChainTasks;   // register budget: one task per wave at J = 8
+  double vsave[TPW], gw[TPW];
+#pragma unroll
+  for (int x = 0; x < TPW; ++x) { vsave[x] = 0.0; gw[x] = 0.0; }
+
+  int slot = 0;
+  for (int g0 = 0; g0 < Bt; g0 += G, slot ^= 1) {
+    // lane id the compiler cannot see through: per-lane addresses are recomputed inside the
+    // loop instead of being hoisted into registers that stay live across it
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    // (a) this wave's staged rows -> registers, then stage the next group behind them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    double p[G][J];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+      for (int jj = 0; jj < J; ++jj)
+        p[gg][jj] = pw[gg * 64 * J + ln + 64 * jj];   // j >= n: finite in-row values, u = 0 there
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if CHAIN_STAGE_AT == 0
+    if (g0 + G < Bt) stage(g0 + G, ln);
+#endif
+    // (b) temp[k,l,row] and 1/temp for the G rows (one Butterfly of R values per row)
+    double* tsl = temp_l + slot * L.TS;
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      double v[NVB];
+#pragma unroll
+      for (int x = 0; x < NVB; ++x) v[x] = 0.0;
+#pragma unroll
+      for (int jj = 0; jj < J; ++jj)
+#pragma unroll
+        for (int l = 0; l < R; ++l) v[l] = fma(p[gg][jj], u[jj][l], v[l]);
+      Butterfly<NVB>::run(v, lane);
+      const int vi = lane >> SHB;
+      if ((lane & ((1 << SHB) - 1)) == 0 && vi < R) {
+        tsl[(k * R + vi) * G + gg] = v[0];
+        tsl[DRG + G + (k * R + vi) * G + gg] = 1.0 / v[0];
+      }
+    }
+    lds_barrier();
+#if CHAIN_STAGE_AT == 1
+    if (g0 + G < Bt) stage(g0 + G, ln);
+#endif
+    // (c) V tasks: task = gg·NCH + c covers q = 64c + lane of batch column g0+gg
+#pragma unroll
+    for (int x = 0; x < TPW; ++x) {
+      const int task = k + D * x;
+      if (task >= L.NT) break;
+      const int gg = task / L.NCH, c = task - gg * L.NCH;
+      const int q = 64 * c + ln;
+      const bool ok = q < Q;
+      const int qq = ok ? q : 0;
+      // every LDS read of the task in flight at once: kChainDMax dimensions, no guards (rows
+      // kk >= D of the tables hit the ones slots / trash rows)
+      int it[kChainDMax], ps[kChainDMax];
+#pragma unroll
+      for (int kk = 0; kk < kChainDMax; ++kk) {
+        it[kk] = IT_l[kk * Q + qq] + gg;
+        ps[kk] = pos_l[kk * Q + qq] + gg * R * kChainRun;
+      }
+      double V = 1.0;                              // Π_k temp in k order (computeV)
+#pragma unroll
+      for (int kk = 0; kk < kChainDMax; ++kk) V *= tsl[it[kk]];
+      const double wV = ok ? w_l[qq] * V : 0.0;
+      if (ok) {
+#pragma unroll
+        for (int kk = 0; kk < kChainDMax; ++kk)    // w_q · V / temp[k] (computeU_phi :253)
+          Lseg[ps[kk]] = wV * tsl[it[kk] + DRG + G];
+      }
+      vsave[x] = ok ? V : 0.0;
+      const double fs = wave_sum(wV);
+      if (lane == 0) fp_l[gg * kChainQPL + c] = fs;
+    }
+    lds_barrier();
+#if CHAIN_STAGE_AT == 2
+    if (g0 + G < Bt) stage(g0 + G, ln);
+#endif
+    // (e) residuals, A[:,k,·]·res, and the gradU / gradw accumulation
+    double res[G];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      double f = 0.0;
+#pragma unroll
+      for (int c = 0; c < kChainQPL; ++c) f += fp_l[gg * kChainQPL + c];   // unused chunks are 0
+      res[gg] = (g0 + gg < Bt) ? y_l[g0 + gg] - f : 0.0;
+    }
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      // A[l,k,row] = Σ of run l of this row's run buffer: one slot per lane and run, then one
+      // Butterfly over the R partial sums
+      double part[NVB];
+      const double* Lp = Lseg + (k * G + gg) * R * kChainRun + ln;
+#pragma unroll
+      for (int x = 0; x < NVB; ++x) part[x] = x < R ? Lp[x * kChainRun] : 0.0;
+      Butterfly<NVB>::run(part, lane);
+#pragma unroll
+      for (int l = 0; l < R; ++l) {
+        const double cc = readlane_d(part[0], l << SHB) * res[gg];
+#pragma unroll
+        for (int jj = 0; jj < J; ++jj) acc[jj][l] = fma(p[gg][jj], cc, acc[jj][l]);
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < TPW; ++x) {
+      const int task = k + D * x;
+      if (task >= L.NT) break;
+      const int gg = task / L.NCH;
+      double rr = res[0];
+#pragma unroll
+      for (int g2 = 1; g2 < G; ++g2) if (gg == g2) rr = res[g2];
+      gw[x] = fma(vsave[x], rr, gw[x]);
+    }
+  }
+  CSTAMP(2);
+
+  const ChainDesc C = *Cp;                 // loaded after the batch loop (see Cp)
+  const double cN = (double)P.N / (double)Bt;
+  const long long post = t - P.burnin_steps;
+  const bool store = post >= 0 && ((post + 1) % P.store_every) == 0;
+  const long long slot_s = store ? (post + 1) / P.store_every - 1 : 0;
+
+  // ---- w: gradw and the Langevin step (GPT_SGLD.jl:393, 411-414)
+#pragma unroll
+  for (int x = 0; x < TPW; ++x) {
+    const int task = k + D * x;
+    if (task >= L.NT) break;
+    gwp_l[task * 64 + lane] = gw[x];
+  }
+  __syncthreads();
+  {
+    const double inv_sw2 = 1.0 / (C.sigma_w * C.sigma_w);
+    const double sqe = sqrt(C.epsw);
+    double gn2 = 0.0;
+#pragma unroll 1
+    for (int q = tid; q < Q; q += NTH) {
+      const int c = q >> 6, ln = q & 63;
+      double g = 0.0;
+      for (int gg = 0; gg < G; ++gg) g += gwp_l[(gg * L.NCH + c) * 64 + ln];
+      const double wq = w_l[q];
+      const double gradw = cN * g / C.signal_var - wq * inv_sw2;
+      double step = C.epsw * gradw / 2;
+      step += sqe * normal_at(C.seed, (uint32_t)q, (uint32_t)t, kWNoise, 0);
+      const double wn = wq + step;
+      gptr_w(C.w)[(size_t)((t + 1) & 1) * Q + q] = wn;
+      if (store && C.w_store) gptr_w(C.w_store)[(size_t)slot_s * Q + q] = wn;
+      gn2 = fma(gradw, gradw, gn2);
+    }
+    if (C.diag) {
+      gn2 = wave_sum(gn2);
+      if (lane == 0) misc[k] = gn2;
+    }
+  }
+  CSTAMP(3);
+
+  // ---- U^(k): gradient, Langevin drive, Stiefel projection + geodesic (per wave)
+  const double cU = cN / C.signal_var;
+  const double sq = sqrt(C.epsU);
+  double gu2 = 0.0;
+  constexpr int RE = R + (R & 1);
+#pragma unroll
+  for (int jj = 0; jj < J; ++jj) {
+    const int j = lane + 64 * jj;
+    // noise pairs through this lane's LDS slots: one non-unrolled Philox/Box–Muller body
+    // (register-light) instead of J·R/2 interleaved copies next to the live U / gradU tiles
+    {
+      const int jc = j < n ? j : n - 1;
+#pragma unroll 1
+      for (int l = 0; l < R; l += 2) {
+        double z0, z1;
+        normal_pair(C.seed, (uint32_t)((l + RE * jc) >> 1), (uint32_t)t, kUNoise, (uint32_t)k, z0, z1);
+        xi_l[lane * RE + l] = z0;
+        xi_l[lane * RE + l + 1] = z1;
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < R; ++l) {
+      const double Gv = j < n ? acc[jj][l] * cU : 0.0;
+      gu2 = fma(Gv, Gv, gu2);
+      acc[jj][l] = j < n ? sq * Gv / 2 + xi_l[lane * RE + l] : 0.0;    // :420 drive
+    }
+  }
+  if (C.diag) {
+    gu2 = wave_sum(gu2);
+    if (lane == 0) C.diag[(size_t)t * (1 + D) + 1 + k] = sqrt(gu2);
+  }
+  CSTAMP(4);
+  {
+    constexpr int NN = 2 * R;
+    constexpr int S0 = (7 * NN * NN > 64 * RE) ? 7 * NN * NN : 64 * RE;
+    double* X0 = X;                          // expm scratch (7·NN²), reused for expm(−tA)
+    double* Ec = X + S0;                     // E[:, 0:r]  (NN × R)
+    double* Mg = Ec + NN * R;                // UᵀW, then Ag | Sg | nrm
+    double* Ag = Mg + R * R;
+    double* Sg = Ag + R * R;
+    double* nr = Sg + R * R;
+    wave_sync();                             // noise slots (aliasing X0) are consumed
+    // proj (GPT_SGLD.jl:14-16): mom = W − U(UᵀW + WᵀU)/2
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      double v[R];
+#pragma unroll
+      for (int bb = 0; bb < R; ++bb) {
+        double s = 0.0;
+#pragma unroll
+        for (int jj = 0; jj < J; ++jj) s = fma(u[jj][a], acc[jj][bb], s);
+        v[bb] = s;
+      }
+      wave_sum_to_lds<R>(v, Mg + a * R);
+    }
+    wave_sync();
+#pragma unroll
+    for (int bb = 0; bb < R; ++bb) {
+      double ms[R];
+#pragma unroll
+      for (int a = 0; a < R; ++a) ms[a] = Mg[a * R + bb] + Mg[bb * R + a];
+#pragma unroll
+      for (int jj = 0; jj < J; ++jj) {
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a < R; ++a) s = fma(u[jj][a], ms[a], s);
+        acc[jj][bb] = acc[jj][bb] - s / 2;
+      }
+    }
+      // geod (GPT_SGLD.jl:19-37): A = Uᵀmom, S = momᵀmom, E = expm(t[A −S; I A]), expm(−tA)
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        double v[2 * R];
+#pragma unroll
+        for (int bb = 0; bb < R; ++bb) {
+          double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+          for (int jj = 0; jj < J; ++jj) {
+            s0 = fma(u[jj][a], acc[jj][bb], s0);
+            s1 = fma(acc[jj][a], acc[jj][bb], s1);
+          }
+          v[bb] = s0;
+          v[R + bb] = s1;
+        }
+        wave_sum_to_lds<R>(v, Ag + a * R, Sg + a * R);
+      }
+      wave_sync();
+      CSTAMP(5);
+      const double tt = sq;
+      for (int o = lane; o < NN * NN; o += 64) {
+        const int i = o / NN, j = o - i * NN;
+        double v;
+        if (i < R) v = j < R ? Ag[i * R + j] : -Sg[i * R + (j - R)];
+        else v = j < R ? (i - R == j ? 1.0 : 0.0) : Ag[(i - R) * R + (j - R)];
+        X0[o] = tt * v;
+      }
+      wave_sync();
+      const bool bad = wave_expm<NN>(X0);
+      for (int o = lane; o < NN * R; o += 64) {
+        const int a = o / R, l = o - a * R;
+        Ec[o] = X0[NN * NN + a * NN + l];
+      }
+      wave_sync();
+      double* X1 = X0;                        // expm(−tA) in the same scratch
+      for (int o = lane; o < R * R; o += 64) X1[o] = -tt * Ag[o];
+      wave_sync();
+      wave_expm<R>(X1);
+      if (bad && lane == 0) flag[0] = 1;
+      CSTAMP(6);
+      const double* mx = X1 + R * R;          // expm(−tA)
+      // F = E[:,1:r]·expm(−tA) (NN × R, on the wave), then tmpU = [U mom]·F row by row
+      // (GPT_SGLD.jl:35 with the two products associated the other way), then normalisation
+      double* F = Mg;                         // grams are dead: reuse their slots
+      wave_sync();
+      for (int o = lane; o < NN * R; o += 64) {
+        const int a = o / R, l = o - a * R;
+        double s = 0.0;
+#pragma unroll
+        for (int c2 = 0; c2 < R; ++c2) s = fma(Ec[a * R + c2], mx[c2 * R + l], s);
+        F[o] = s;
+      }
+      wave_sync();
+      // two passes with R×R halves of F in registers: U·F[0:r,:] in place, then += mom·F[r:2r,:]
+      // (each F value read from LDS once per wave)
+      {
+        double Fh[R * R];
+#pragma unroll
+        for (int x = 0; x < R * R; ++x) Fh[x] = F[x];
+#pragma unroll
+        for (int jj = 0; jj < J; ++jj) {
+          double o[R];
+#pragma unroll
+          for (int l = 0; l < R; ++l) o[l] = 0.0;
+#pragma unroll
+          for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int l = 0; l < R; ++l) o[l] = fma(u[jj][a], Fh[a * R + l], o[l]);
+#pragma unroll
+          for (int l = 0; l < R; ++l) u[jj][l] = o[l];
+        }
+      }
+      double nrm[R];
+#pragma unroll
+      for (int l = 0; l < R; ++l) nrm[l] = 0.0;
+      {
+        double Fh[R * R];
+#pragma unroll
+        for (int x = 0; x < R * R; ++x) Fh[x] = F[R * R + x];
+#pragma unroll
+        for (int jj = 0; jj < J; ++jj) {
+#pragma unroll
+          for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int l = 0; l < R; ++l) u[jj][l] = fma(acc[jj][a], Fh[a * R + l], u[jj][l]);
+#pragma unroll
+          for (int l = 0; l < R; ++l) nrm[l] = fma(u[jj][l], u[jj][l], nrm[l]);
+        }
+      }
+      wave_sum_to_lds<R>(nrm, nr);
+      wave_sync();
+#pragma unroll
+      for (int l = 0; l < R; ++l) {
+        const double isc = 1.0 / sqrt(nr[l]);
+#pragma unroll
+        for (int jj = 0; jj < J; ++jj) u[jj][l] = u[jj][l] * isc;
+      }
+    }
+    if (P.stamps && lane == 0)            // per-wave arrival at the end-of-step barrier (diag)
+    P.stamps[(size_t)blockIdx.x * kStamps + 8 + k] = (long long)__builtin_amdgcn_s_memtime();
+  __syncthreads();                      // w_l, flag and the gradw partials are complete
+    if (C.diag && tid == 0) {
+      double s = 0.0;
+      for (int w2 = 0; w2 < D; ++w2) s += misc[w2];
+      C.diag[(size_t)t * (1 + D)] = sqrt(s);
+    }
+    if (flag[0]) {                        // NaN in the geodesic: the chain stops (:422-424)
+      if (tid == 0) __hip_atomic_store(C.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    double* Uk = C.U + (size_t)n * R * k;
+    double* Us = (store && C.U_store) ? C.U_store + ((size_t)slot_s * D + k) * n * R : nullptr;
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = lane + 64 * jj;
+      if (j < n)
+#pragma unroll
+        for (int l = 0; l < R; ++l) {
+          gptr_w(Uk)[j + (size_t)n * l] = u[jj][l];
+          if (Us) gptr_w(Us)[j + (size_t)n * l] = u[jj][l];
+        }
+    }
+    CSTAMP(7);
+}
+
+// ------------------------------------------------------------------------------ host side
+#define GPT_CHAIN_CFGS(X) \
+  X(1, 1) X(1, 2) X(1, 4) X(1, 8) X(2, 1) X(2, 2) X(2, 4) X(2, 8) X(3, 1) X(3, 2) X(3, 4) X(3, 8) \
+  X(4, 1) X(4, 2) X(4, 4) X(4, 8) X(5, 1) X(5, 2) X(5, 4) X(5, 8)
+
+// Static LDS of chain_kernel<R, J, G>: the row staging buffer.
+static size_t chain_static_lds(int J) { return 8 * (size_t)kChainDMax * kChainG * 64 * J; }
+
+static int chain_J(int n) { return n <= 64 ? 1 : (n <= 128 ? 2 : (n <= 256 ? 4 : (n <= 512 ? 8 : 0))); }
+
+size_t chain_lds_bytes(int n, int D, int r, int Q, int m) {
+  return chain_layout(n, D, r, Q, m, kChainG).bytes;
+}
+
+bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stiefel, int max_run) {
+  if (max_run > kChainRun) return false;  // a run of core entries must fit its 64 slots
+  if (!langevin || !stiefel) return false;   // SGD / Euclidean variants run on the grid engine
+  if (D < 1 || D > kChainDMax || r < 1 || r > 5 || chain_J(n) == 0) return false;
+  if (chain_J(n) >= 2 && (n & 1)) return false;   // 16-B row staging needs 16-B aligned rows
+  const ChainLayout L = chain_layout(n, D, r, Q, m, kChainG);
+  if (Q > kChainQP) return false;
+  if (L.NT > (chain_J(n) >= 8 ? 1 : kChainTasks) * D) return false;
+  return L.bytes + chain_static_lds(chain_J(n)) <= 160 * 1024;
+}
+
+hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchains,
+                        const long long* tbase, int t_local, hipStream_t st) {
+  const int J = chain_J(P.n);
+  const size_t lds = chain_lds_bytes(P.n, P.D, P.r, P.Q, P.m);
+  dim3 grid(nchains), block(64 * P.D);
+#define CASE(RR, JJ)                                                                          \
+  if (P.r == RR && J == JJ) {                                                                 \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      hipError_t e = hipFuncSetAttribute((const void*)chain_kernel<RR, JJ, kChainG>,          \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,          \
+                                         (int)(160 * 1024 - chain_static_lds(JJ)));           \
+      if (e != hipSuccess) return e;                                                          \
+      attr = true;                                                                            \
+    }                                                                                         \
+    hipLaunchKernelGGL((chain_kernel<RR, JJ, kChainG>), grid, block, lds, st, P, chains, tbase, t_local); \
+    return hipGetLastError();                                                                 \
+  }
+  GPT_CHAIN_CFGS(CASE)
+#undef CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace gpt

@@ -5,6 +5,14 @@
 namespace gpt {
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// A pointer known to be wave-uniform, held in SGPRs.
+template <class T>
+__device__ __forceinline__ T* uni_ptr(T* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (T*)(((unsigned long long)hi << 32) | lo);
+}
 
 // Order LDS traffic between the lanes of ONE wave (no workgroup barrier).
 __device__ __forceinline__ void wave_sync() {
@@ -13,10 +21,66 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- cross-lane exchanges without LDS (gfx950): v_permlane32/16_swap and DPP row/quad moves.
+// xch<OFF>(a, b): lane λ returns a(λ) + [partner's b] where λ keeps a and sends b (partner of λ at
+// "distance" OFF; for OFF = 4 the partner is the row_half_mirror lane, which also differs in bit 2).
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int OFF>
+__device__ __forceinline__ double dpp_partner(double v) {
+  static_assert(OFF == 8 || OFF == 4 || OFF == 2 || OFF == 1, "DPP partner offset");
+  if constexpr (OFF == 8) return dpp_d<0x128>(v);        // row_ror:8   (λ ^ 8 within a row)
+  else if constexpr (OFF == 4) return dpp_d<0x141>(v);   // row_half_mirror (bit 2 flips)
+  else if constexpr (OFF == 2) return dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+  else return dpp_d<0xB1>(v);                            // quad_perm [1,0,3,2]
+}
+// Pair exchange for the halving butterfly round at lane bit OFF: lanes with the bit clear keep
+// `lo` and receive the partner's `lo`; lanes with it set keep `hi` and receive the partner's
+// `hi`; returns keep + received.
+template <int OFF>
+__device__ __forceinline__ double pair_sum(double lo, double hi, int lane) {
+  if constexpr (OFF == 32 || OFF == 16) {
+    const long long a = __double_as_longlong(lo), b = __double_as_longlong(hi);
+    unsigned al = (unsigned)a, ah = (unsigned)(a >> 32), bl = (unsigned)b, bh = (unsigned)(b >> 32);
+    if constexpr (OFF == 32) {
+      auto l2 = __builtin_amdgcn_permlane32_swap(al, bl, false, false);
+      auto h2 = __builtin_amdgcn_permlane32_swap(ah, bh, false, false);
+      al = l2[0]; bl = l2[1]; ah = h2[0]; bh = h2[1];
+    } else {
+      auto l2 = __builtin_amdgcn_permlane16_swap(al, bl, false, false);
+      auto h2 = __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
+      al = l2[0]; bl = l2[1]; ah = h2[0]; bh = h2[1];
+    }
+    // lower half now holds (own lo, partner lo), upper half (partner hi, own hi)
+    return __longlong_as_double(((long long)ah << 32) | al) +
+           __longlong_as_double(((long long)bh << 32) | bl);
+  } else {
+    const bool up = (lane & OFF) != 0;
+    const double send = up ? lo : hi;
+    const double keep = up ? hi : lo;
+    return keep + dpp_partner<OFF>(send);
+  }
+}
+// v + partner's v (single-value round).
+template <int OFF>
+__device__ __forceinline__ double self_sum(double v, int lane) {
+  if constexpr (OFF == 32 || OFF == 16) return pair_sum<OFF>(v, v, lane);
+  else return v + dpp_partner<OFF>(v);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  const int lane = threadIdx.x & 63;
+  v = self_sum<32>(v, lane);
+  v = self_sum<16>(v, lane);
+  v = self_sum<8>(v, lane);
+  v = self_sum<4>(v, lane);
+  v = self_sum<2>(v, lane);
+  return self_sum<1>(v, lane);
 }
 
 __device__ __forceinline__ double wave_max(double v) {
@@ -52,16 +116,11 @@ struct Butterfly {
     if constexpr (S < P) {
       constexpr int off = 32 >> S;
       constexpr int h = NV >> (S + 1);
-      const bool up = (lane & off) != 0;
 #pragma unroll
-      for (int u = 0; u < h; ++u) {
-        const double send = up ? v[u] : v[u + h];
-        const double keep = up ? v[u + h] : v[u];
-        v[u] = keep + __shfl_xor(send, off, 64);
-      }
+      for (int u = 0; u < h; ++u) v[u] = pair_sum<off>(v[u], v[u + h], lane);
       round<S + 1>(v, lane);
     } else if constexpr (S < 6) {
-      v[0] += __shfl_xor(v[0], 32 >> S, 64);
+      v[0] = self_sum<(32 >> S)>(v[0], lane);
       round<S + 1>(v, lane);
     }
   }

@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #define GPT_HD __host__ __device__ __forceinline__
+#include "fastmath.h"
 
 namespace gpt {
 
@@ -37,13 +38,28 @@ GPT_HD double u53(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6) + 0.5) * (1.0 / 9007199254740992.0);
 }
 
+__constant__ double kFmCoef[23] = GPT_FM_COEF;
+
+// The Box–Muller coefficient table behind a pointer the compiler cannot see through: the
+// coefficients are scalar-loaded where used rather than hoisted into registers.
+__device__ __forceinline__ const __attribute__((address_space(4))) double* fm_coef() {
+  const __attribute__((address_space(4))) double* c =
+      (const __attribute__((address_space(4))) double*)kFmCoef;
+  asm volatile("" : "+s"(c));
+  return c;
+}
+
 // Element e of normal stream (c1, c2, c3): Box–Muller on the block at c0 = e>>1.
-GPT_HD double normal_at(uint64_t seed, uint32_t e, uint32_t c1, uint32_t c2, uint32_t c3) {
+// (log / sincos(2πu) from fastmath.h; host-side draws use libm in capi.hip.)
+__device__ __forceinline__ double normal_at(uint64_t seed, uint32_t e, uint32_t c1, uint32_t c2,
+                                            uint32_t c3) {
   const U4 x = philox4x32(e >> 1, c1, c2, c3, seed);
   const double u1 = u53(x.x, x.y), u2 = u53(x.z, x.w);
-  const double rad = sqrt(-2.0 * log(u1));
-  const double th = 6.283185307179586 * u2;   // 2π·u2 (2.0*np.pi*u2 in the oracle)
-  return (e & 1u) ? rad * sin(th) : rad * cos(th);
+  const auto c = fm_coef();
+  const double rad = sqrt(-2.0 * fm_log_c(u1, c));
+  double sn, cs;
+  fm_sincos_2pi_c(u2, sn, cs, c);
+  return (e & 1u) ? rad * sn : rad * cs;
 }
 
 // Both Box–Muller outputs of the block at c0 (elements 2·c0 and 2·c0+1 of the stream).
@@ -51,9 +67,10 @@ __device__ __forceinline__ void normal_pair(uint64_t seed, uint32_t c0, uint32_t
                                             uint32_t c3, double& z0, double& z1) {
   const U4 x = philox4x32(c0, c1, c2, c3, seed);
   const double u1 = u53(x.x, x.y), u2 = u53(x.z, x.w);
-  const double rad = sqrt(-2.0 * log(u1));
+  const auto c = fm_coef();
+  const double rad = sqrt(-2.0 * fm_log_c(u1, c));
   double sn, cs;
-  sincos(6.283185307179586 * u2, &sn, &cs);
+  fm_sincos_2pi_c(u2, sn, cs, c);
   z0 = rad * cs;
   z1 = rad * sn;
 }

@@ -9,9 +9,17 @@
 
 namespace gpt {
 
-constexpr int kNT = 512;           // threads per workgroup (8 waves of 64)
+#ifndef GPT_NT
+#define GPT_NT 512
+#endif
+#ifndef GPT_WPE
+#define GPT_WPE 2
+#endif
+constexpr int kNT = GPT_NT;        // threads per workgroup (waves of 64)
 constexpr int kNW = kNT / 64;      // waves per workgroup
 constexpr int kDMax = 16;          // max input dimensions D handled by the kernels
+constexpr int kEngineGrid = 0;     // sgld.hip: grid (D+1, chains), two batch reads per step
+constexpr int kEngineChain = 1;    // chain.hip: one workgroup per chain, one batch read per step
 
 // Per-chain device state.  All pointers are device pointers.
 struct ChainDesc {
@@ -36,6 +44,8 @@ struct StepParams {
   int store_every;
   int langevin, stiefel;
   const int32_t* I0;              // Q*D 0-based, layout q + Q*k
+  const int32_t* segpos;          // chain engine: pos (Q*D, rank of q in the (I[q,k], q) order of
+                                  // dimension k, layout q + Q*k) then seg (D*(r+1) run starts)
   long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
 };
 constexpr int kStamps = 16;       // stamp slots per block
@@ -110,6 +120,13 @@ hipError_t launch_step(const StepParams& P, const ChainDesc* chains, int nchains
                        const long long* tbase, int t_local, hipStream_t st);
 hipError_t launch_advance(long long* tbase, long long by, hipStream_t st);
 bool rank_supported(int r);
+
+// Chain-resident engine (chain.hip): one workgroup per chain, many steps per launch.
+bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stiefel,
+                     int max_run = 0);
+size_t chain_lds_bytes(int n, int D, int r, int Q, int m);
+hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchains,
+                        const long long* tbase, int t_local, hipStream_t st);
 
 hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, const double* phitest,
                        int n, int D, long long Ntest, int r, int Q, int S, double* fhat,

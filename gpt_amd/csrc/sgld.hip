@@ -25,7 +25,7 @@ namespace gpt {
   } while (0)
 
 template <int R>
-__global__ __launch_bounds__(kNT) void sgld_step_kernel(StepParams P,
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) void sgld_step_kernel(StepParams P,
                                                         const ChainDesc* __restrict__ chains,
                                                         const long long* __restrict__ tbase,
                                                         int t_local) {
@@ -353,7 +353,6 @@ __global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
   const int n = P.n, D = P.D, m = P.m;
   const StepLayout L = step_layout(n, D, R, P.Q, m);
   const int NP = L.NP, NS = L.NS;
-  int* idx_l = (int*)(smem + L.o_idx);
   double* U_l = (double*)(smem + L.o_U);
   const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
   const int start = b * m;

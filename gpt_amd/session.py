@@ -14,10 +14,15 @@ from ._lib import SGLDConfig, check, lib
 from .GPT_SGLD import make_config
 
 
+# store_flags bits selecting the step engine (include/gptsgld.h, gpt_sgld_session_info)
+ENGINES = {"auto": 0, "grid": 4, "chain": 8}
+ENGINE_NAMES = {0: "grid", 1: "chain"}
+
+
 class SGLDSession:
     def __init__(self, phis, ys, I, r, Q, m, epsw, epsU, signal_var, burnin, maxepoch, seeds,
                  sigma_w=1.0, langevin=True, stiefel=True, store_every=1, max_steps=0,
-                 store=True, diag=False, stream=None):
+                 store=True, diag=False, stream=None, engine="auto"):
         import torch
         if not isinstance(phis, (list, tuple)):
             phis = [phis]
@@ -46,7 +51,9 @@ class SGLDSession:
         yy = (C.c_void_p * nch)(*[y.data_ptr() for y in ys])
         sd = (C.c_uint64 * nch)(*[int(s) & (2 ** 64 - 1) for s in seeds])
         h = C.c_void_p()
-        flags = (1 if store else 0) | (2 if diag else 0)
+        if engine not in ENGINES:
+            raise ValueError("engine must be one of %s" % sorted(ENGINES))
+        flags = (1 if store else 0) | (2 if diag else 0) | ENGINES[engine]
         st = C.c_void_p(stream) if stream else None
         check(lib().gpt_sgld_session_create(C.byref(self.cfg), nch, sd, pp, yy,
                                             I.ctypes.data_as(_lib.P_I32), flags, st, C.byref(h)))
@@ -69,6 +76,13 @@ class SGLDSession:
         avg = C.c_double(0.0)
         check(lib().gpt_sgld_session_time_steps(self._h, int(nsteps), C.byref(avg)))
         return avg.value
+
+    def info(self):
+        """dict(engine, lds_bytes, threads, workgroups) of the step launch."""
+        out = (C.c_int64 * 4)()
+        check(lib().gpt_sgld_session_info(self._h, out))
+        return dict(engine=ENGINE_NAMES.get(out[0], str(out[0])), lds_bytes=out[1],
+                    threads=out[2], workgroups=out[3])
 
     def sync(self):
         check(lib().gpt_sgld_session_sync(self._h))

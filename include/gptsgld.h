@@ -112,6 +112,12 @@ int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out);
 int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double* w_store, double* U_store,
                            double* diag, int32_t* status);
 void gpt_sgld_session_destroy(gpt_sgld_session* s);
+/* out[4] = {engine (0 grid: D+1 workgroups per chain, 1 chain: one workgroup per chain),
+ *           LDS bytes per workgroup, threads per workgroup, workgroups per step launch}.
+ * store_flags of gpt_sgld_session_create: bit0 stores, bit1 diagnostics, bit2 force the grid
+ * engine, bit3 force the chain engine (default: chain whenever the shape allows it; the
+ * environment variable GPTSGLD_ENGINE=grid|chain overrides the default). */
+int gpt_sgld_session_info(gpt_sgld_session* s, int64_t* out);
 
 /* ---- prediction ---------------------------------------------------------------------- */
 /* pred(w,U,I,phitest)  GPT_SGLD.jl:233-243  -> fhat (Ntest) */

@@ -13,6 +13,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+CHAIN_NAMES = {1: "prologue (tables, U, rows)", 2: "batch loop", 3: "w update",
+               4: "U noise + drive", 5: "proj + geod grams", 6: "expm x2", 7: "tmpU, norm, U write"}
 NAMES = {1: "P0 stage", 2: "P1 V-phase", 3: "w-block gradw / U stage", 4: "P2 gradU+noise",
          5: "proj gram+mom", 6: "geod grams", 7: "expm x2", 8: "tmpU+norm", 9: "U write+idx",
          10: "P5 next temp"}
@@ -27,6 +29,7 @@ def main():
     ap.add_argument("--m", type=int, default=50)
     ap.add_argument("--sgd", action="store_true", help="langevin=False (no noise draws)")
     ap.add_argument("--N", type=int, default=10000, help="training rows used (phi footprint)")
+    ap.add_argument("--engine", default="grid", choices=["grid", "chain"])
     args = ap.parse_args()
     import torch
     import bench
@@ -44,9 +47,29 @@ def main():
     phi = feature_device(tt(Xtr.T), tt(ls), 1.042, math.sqrt(n / Q ** (1 / D)), tt(Z.T), tt(b.T))
     y = tt(ytr)
     s = SGLDSession(phi, y, I, r, Q, m, 1e-5, 1e-8, 0.0476, 0, 3, list(range(1, args.chains + 1)),
-                    store=False, langevin=not args.sgd)
+                    store=False, langevin=not args.sgd, engine=args.engine)
     s.run(50)
     s.sync()
+    if args.engine == "chain":
+        # the library sizes every step's slice for D+1 workgroups per chain; chain-engine
+        # workgroup c writes slot c of it
+        out = np.zeros((args.steps, (D + 1) * args.chains, 16), dtype=np.int64)
+        check(lib().gpt_sgld_session_stamps(s._h, args.steps, out.ctypes.data_as(C.POINTER(C.c_int64))))
+        out = out[:, :args.chains, :]
+        tot = np.median((out[..., 7] - out[..., 0]).ravel())
+        print("chain engine: median cycles per phase (wave 0), batch of %d rows" % m)
+        order = [1, 2, 3, 4, 5, 6, 7]
+        prev = 0
+        for i in order:
+            v = np.median((out[..., i] - out[..., prev]).ravel())
+            print("  %2d %-28s %8.0f cyc  %5.1f%%" % (i, CHAIN_NAMES[i], v, 100 * v / tot))
+            prev = i
+        print("  total %.0f cycles" % tot)
+        arr = out[..., 8:16] - out[..., 0:1]
+        print("  per-wave arrival at the end-of-step barrier (cycles from start):",
+              " ".join("%d" % v for v in np.median(arr.reshape(-1, 8), axis=0)))
+        print("event-timed step kernel: %.2f us" % s.time_steps(20))
+        return
     nb = (D + 1) * args.chains
     out = np.zeros((args.steps, nb, 16), dtype=np.int64)
     check(lib().gpt_sgld_session_stamps(s._h, args.steps, out.ctypes.data_as(C.POINTER(C.c_int64))))

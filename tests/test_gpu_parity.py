@@ -111,14 +111,24 @@ CASES = {
 }
 
 
-@pytest.mark.parametrize("name", list(CASES))
-def test_sampler_trajectory_matches_oracle(name):
+def _chain_ok(n, D, r, lang, stf):
+    """Shapes the chain engine (chain.hip) takes; the grid engine (sgld.hip) takes all."""
+    return lang and stf and D <= 8 and r <= 5 and n <= 512
+
+
+ENGINE_CASES = [(name, eng) for name in CASES for eng in ("grid", "chain")
+                if eng == "grid" or _chain_ok(*[CASES[name][i] for i in (0, 1, 3, 9, 10)])]
+
+
+@pytest.mark.parametrize("name,engine", ENGINE_CASES)
+def test_sampler_trajectory_matches_oracle(name, engine):
     n, D, N, r, Q, m, burnin, maxepoch, se, lang, stf = CASES[name]
     p = make_problem(n, D, N, r, Q, seed=11)
-    kw = dict(langevin=lang, stiefel=stf, store_every=se)
+    kw = dict(langevin=lang, stiefel=stf, store_every=se, engine=engine)
     epsw, epsU, sv, seed = 1e-4, 1e-6, 0.05, 23
     ws, Us, dg = G().GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
                                    maxepoch, seed, diag=True, **kw)
+    kw.pop("engine")
     wo, Uo, info = R.GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
                                    maxepoch, seed, record=True, **kw)
     assert info["status"] == 0
@@ -143,23 +153,26 @@ def test_sgldERM_generation_a_mapping():
     assert rel(ws, wo) < 1e-8 and rel(Us, Uo) < 1e-8
 
 
-def test_injected_initial_state():
+@pytest.mark.parametrize("engine", ["grid", "chain"])
+def test_injected_initial_state(engine):
     n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
     p = make_problem(n, D, N, r, Q, seed=8)
     rng = np.random.default_rng(0)
     w0 = rng.standard_normal(Q)
     _, U0 = R.init_state(n, r, D, Q, 999)
     ws, Us = G().GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e-6, 0, 1, 4,
-                               w_init=w0, U_init=U0)
+                               w_init=w0, U_init=U0, engine=engine)
     wo, Uo, _ = R.GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e-6, 0, 1, 4,
                                 w_init=w0, U_init=U0)
     assert rel(ws, wo) < 1e-8 and rel(Us, Uo) < 1e-8
 
 
-def test_nan_geodesic_bailout_zero_fills(capsys):
+@pytest.mark.parametrize("engine", ["grid", "chain"])
+def test_nan_geodesic_bailout_zero_fills(capsys, engine):
     n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
     p = make_problem(n, D, N, r, Q, seed=6)
-    ws, Us = G().GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e300, 0, 2, 3)
+    ws, Us = G().GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e300, 0, 2, 3,
+                               engine=engine)
     assert not ws.any() and not Us.any()
     assert "Get NaN when moving along Geodesic" in capsys.readouterr().out
     _, _, info = R.GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e300, 0, 2, 3)
@@ -187,7 +200,8 @@ def test_gpnt_sgld_matches_oracle():
     assert rel(got, want) < 1e-9
 
 
-def test_multichain_session_equals_single_runs():
+@pytest.mark.parametrize("engine", ["grid", "chain"])
+def test_multichain_session_equals_single_runs(engine):
     import torch
     from gpt_amd.session import SGLDSession
     n, D, N, r, Q, m = 32, 4, 60, 3, 12, 16
@@ -195,7 +209,9 @@ def test_multichain_session_equals_single_runs():
     phi_t = torch.from_numpy(np.ascontiguousarray(p["phi"].transpose(2, 1, 0))).cuda()
     y_t = torch.from_numpy(p["y"]).cuda()
     seeds = [3, 4, 5]
-    s = SGLDSession(phi_t, y_t, p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 2, seeds, store_every=2)
+    s = SGLDSession(phi_t, y_t, p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 2, seeds, store_every=2,
+                    engine=engine)
+    assert s.info()["engine"] == engine
     s.run(3)          # partial chunk, then the rest through the captured graph
     s.run(10 ** 9)
     s.sync()
