@@ -20,8 +20,17 @@
 
 namespace gpt {
 
+#ifndef CHAIN_EXP_NOSTAGE        // diagnostics only (wrong results): skip the row DMA / V tasks
+#define CHAIN_EXP_NOSTAGE 0
+#endif
+#ifndef CHAIN_EXP_NOV
+#define CHAIN_EXP_NOV 0
+#endif
+#ifndef CHAIN_ITREG              // V-task table entries held in registers across the batch
+#define CHAIN_ITREG 1
+#endif
 #ifndef CHAIN_STAGE_AT
-#define CHAIN_STAGE_AT 2          // where the next group's rows are staged: 0 (a), 1 (c), 2 (e)
+#define CHAIN_STAGE_AT 3          // next group's rows staged at: 0 (a), 1 (c), 2 (e), 3 end of (b), 4 end of (c)
 #endif
 constexpr int kChainDMax = 8;     // waves per workgroup (one per input dimension)
 constexpr int kChainTasks = 2;    // V-phase tasks per wave (NCH·G <= tasks·D); J = 8: 1
@@ -29,6 +38,8 @@ constexpr int kChainG = 2;        // batch rows per group
 constexpr int kChainQPL = 4;      // q chunks of 64 (Q <= 64·kChainQPL)
 constexpr int kChainQP = 64 * kChainQPL;
 constexpr int kChainRun = 64;     // slots per run (core entries with one value of I[·,k]) per row
+constexpr int kChainRunS = 72;    // run stride (doubles): 8-lane readers of runs l, l+1.. hit
+                                  // disjoint LDS bank ranges (72·2 dwords ≡ 16 banks mod 64)
 
 struct ChainLayout {
   int NCH, NT;                    // q chunks of 64, tasks = NCH·G
@@ -61,7 +72,8 @@ GPT_HD ChainLayout chain_layout(int n, int D, int r, int Q, int m, int G) {
   L.o_gwp = o;  o = al16(o + 8 * (size_t)L.NT * 64);
   L.o_misc = o; o = al16(o + 8 * 16);
   L.o_un = o;
-  L.L_dbl = (size_t)kChainDMax * G * r * kChainRun;            // runs: [k][row][l][slot]
+  // batch-loop tenants: runs [k][row][l][slot] (stride kChainRunS) | per-wave reduction scratch
+  L.L_dbl = (size_t)kChainDMax * G * r * kChainRunS + (size_t)D * r * kChainRunS;
   L.x_dbl = chain_scratch_dbl(r);
   const size_t un = 8 * (L.L_dbl > L.x_dbl * D ? L.L_dbl : L.x_dbl * D);
   L.bytes = al16(o + un);
@@ -138,6 +150,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   double* X = (double*)(smem + L.o_un) + (size_t)k * L.x_dbl;   // this wave's scratch
   double* xi_l = X;                                             // noise slots (before expm)
   double* pw = pbuf + k * (G * 64 * J);                         // this wave's staged rows
+  double* bscr = Lseg + (size_t)kChainDMax * G * R * kChainRunS + (size_t)k * R * kChainRunS;
 
   const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
@@ -156,14 +169,14 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       if (kk < D) {
         const int l = gptr(P.I0)[q + Q * kk];
         IT_l[o] = (kk * R + l) * G;
-        pos_l[o] = (kk * G * R + l) * kChainRun +
+        pos_l[o] = (kk * G * R + l) * kChainRunS +
                    (gptr(P.segpos)[q + Q * kk] - gptr(segp)[kk * (R + 1) + l]);
       } else {
         IT_l[o] = DRG;
-        pos_l[o] = kk * G * R * kChainRun;
+        pos_l[o] = kk * G * R * kChainRunS;
       }
     }
-    for (int o = tid; o < D * G * R * kChainRun; o += NTH) Lseg[o] = 0.0;   // empty slots read 0
+    for (int o = tid; o < D * G * R * kChainRunS; o += NTH) Lseg[o] = 0.0;  // empty slots read 0
     for (int o = tid; o < 2 * G; o += NTH) {                     // ones slots of both temp slots
       temp_l[o / G * L.TS + DRG + o % G] = 1.0;
       temp_l[o / G * L.TS + 2 * DRG + G + o % G] = 1.0;
@@ -237,8 +250,6 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   };
   stage(0, lane);
 
-  constexpr int NVB = R <= 8 ? 8 : (R <= 16 ? 16 : (R <= 32 ? 32 : 64));
-  constexpr int SHB = 6 - Butterfly<NVB>::P;
 
   double acc[J][R];
 #pragma unroll
@@ -250,6 +261,19 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #pragma unroll
   for (int x = 0; x < TPW; ++x) { vsave[x] = 0.0; gw[x] = 0.0; }
 
+#if CHAIN_ITREG
+  // this wave's V-task table entries, packed (temp index | run slot << 12), fixed for the step
+  int itps[TPW][kChainDMax];
+#pragma unroll
+  for (int x = 0; x < TPW; ++x) {
+    const int task = k + D * x;
+    const int c = task < L.NT ? task % L.NCH : 0;
+    const int qq = min(64 * c + lane, Q - 1);
+#pragma unroll
+    for (int kk = 0; kk < kChainDMax; ++kk)
+      itps[x][kk] = IT_l[kk * Q + qq] | (pos_l[kk * Q + qq] << 12);
+  }
+#endif
   int slot = 0;
   for (int g0 = 0; g0 < Bt; g0 += G, slot ^= 1) {
     // lane id the compiler cannot see through: per-lane addresses are recomputed inside the
@@ -268,24 +292,34 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #if CHAIN_STAGE_AT == 0
     if (g0 + G < Bt) stage(g0 + G, ln);
 #endif
-    // (b) temp[k,l,row] and 1/temp for the G rows (one Butterfly of R values per row)
+    // (b) temp[k,l,row] and 1/temp for the G rows: R partial dots per lane, reduced through this
+    // wave's LDS scratch by 8-lane groups (lane 8l+s sums 8 partials of output l, DPP finishes)
     double* tsl = temp_l + slot * L.TS;
+    const int rl = min(ln >> 3, R - 1), rs = ln & 7;
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
-      double v[NVB];
+      double v[R];
 #pragma unroll
-      for (int x = 0; x < NVB; ++x) v[x] = 0.0;
+      for (int l = 0; l < R; ++l) v[l] = 0.0;
 #pragma unroll
       for (int jj = 0; jj < J; ++jj)
 #pragma unroll
         for (int l = 0; l < R; ++l) v[l] = fma(p[gg][jj], u[jj][l], v[l]);
-      Butterfly<NVB>::run(v, lane);
-      const int vi = lane >> SHB;
-      if ((lane & ((1 << SHB) - 1)) == 0 && vi < R) {
-        tsl[(k * R + vi) * G + gg] = v[0];
-        tsl[DRG + G + (k * R + vi) * G + gg] = 1.0 / v[0];
+#pragma unroll
+      for (int l = 0; l < R; ++l) bscr[l * kChainRunS + ln] = v[l];
+      wave_sync();
+      double sacc = 0.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sacc += bscr[rl * kChainRunS + rs + 8 * i];
+      sacc = group8_sum(sacc);
+      if (rs == 0 && (ln >> 3) < R) {
+        tsl[(k * R + rl) * G + gg] = sacc;
+        tsl[DRG + G + (k * R + rl) * G + gg] = 1.0 / sacc;
       }
     }
+#if CHAIN_STAGE_AT == 3
+    if (g0 + G < Bt) stage(g0 + G, ln);
+#endif
     lds_barrier();
 #if CHAIN_STAGE_AT == 1
     if (g0 + G < Bt) stage(g0 + G, ln);
@@ -294,7 +328,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #pragma unroll
     for (int x = 0; x < TPW; ++x) {
       const int task = k + D * x;
-      if (task >= L.NT) break;
+      if (task >= L.NT || CHAIN_EXP_NOV) break;
       const int gg = task / L.NCH, c = task - gg * L.NCH;
       const int q = 64 * c + ln;
       const bool ok = q < Q;
@@ -302,11 +336,19 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       // every LDS read of the task in flight at once: kChainDMax dimensions, no guards (rows
       // kk >= D of the tables hit the ones slots / trash rows)
       int it[kChainDMax], ps[kChainDMax];
+#if CHAIN_ITREG
+#pragma unroll
+      for (int kk = 0; kk < kChainDMax; ++kk) {
+        it[kk] = (itps[x][kk] & 0xfff) + gg;
+        ps[kk] = (itps[x][kk] >> 12) + gg * R * kChainRunS;
+      }
+#else
 #pragma unroll
       for (int kk = 0; kk < kChainDMax; ++kk) {
         it[kk] = IT_l[kk * Q + qq] + gg;
-        ps[kk] = pos_l[kk * Q + qq] + gg * R * kChainRun;
+        ps[kk] = pos_l[kk * Q + qq] + gg * R * kChainRunS;
       }
+#endif
       double V = 1.0;                              // Π_k temp in k order (computeV)
 #pragma unroll
       for (int kk = 0; kk < kChainDMax; ++kk) V *= tsl[it[kk]];
@@ -320,9 +362,12 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       const double fs = wave_sum(wV);
       if (lane == 0) fp_l[gg * kChainQPL + c] = fs;
     }
+#if CHAIN_STAGE_AT == 4
+    if (g0 + G < Bt) stage(g0 + G, ln);
+#endif
     lds_barrier();
 #if CHAIN_STAGE_AT == 2
-    if (g0 + G < Bt) stage(g0 + G, ln);
+    if (!CHAIN_EXP_NOSTAGE && g0 + G < Bt) stage(g0 + G, ln);
 #endif
     // (e) residuals, A[:,k,·]·res, and the gradU / gradw accumulation
     double res[G];
@@ -335,16 +380,16 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
     }
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
-      // A[l,k,row] = Σ of run l of this row's run buffer: one slot per lane and run, then one
-      // Butterfly over the R partial sums
-      double part[NVB];
-      const double* Lp = Lseg + (k * G + gg) * R * kChainRun + ln;
+      // A[l,k,row] = Σ of run l of this row's run slots: lane 8l+s sums slots s, s+8, ..., the
+      // 8-lane group finishes with DPP; lane 8l then holds A[l]
+      const double* Lp = Lseg + ((k * G + gg) * R + rl) * kChainRunS + rs;
+      double a = 0.0;
 #pragma unroll
-      for (int x = 0; x < NVB; ++x) part[x] = x < R ? Lp[x * kChainRun] : 0.0;
-      Butterfly<NVB>::run(part, lane);
+      for (int i = 0; i < 8; ++i) a += Lp[8 * i];
+      a = group8_sum(a);
 #pragma unroll
       for (int l = 0; l < R; ++l) {
-        const double cc = readlane_d(part[0], l << SHB) * res[gg];
+        const double cc = readlane_d(a, 8 * l) * res[gg];
 #pragma unroll
         for (int jj = 0; jj < J; ++jj) acc[jj][l] = fma(p[gg][jj], cc, acc[jj][l]);
       }

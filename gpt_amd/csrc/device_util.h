@@ -73,6 +73,13 @@ __device__ __forceinline__ double self_sum(double v, int lane) {
   else return v + dpp_partner<OFF>(v);
 }
 
+// Sum over aligned groups of 8 lanes (every lane of the group gets it): DPP only.
+__device__ __forceinline__ double group8_sum(double v) {
+  v += dpp_partner<1>(v);
+  v += dpp_partner<2>(v);
+  return v + dpp_partner<4>(v);     // row_half_mirror pairs the two quads of the group
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
   const int lane = threadIdx.x & 63;
   v = self_sum<32>(v, lane);
