@@ -210,6 +210,40 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
     return (w_store, U_store, dg) if diag else (w_store, U_store)
 
 
+def GPT_SGLDERM_RMSprop(phi, y, signal_var, I, r, Q, m, epsilon, alpha, burnin, maxepoch,
+                        param_seed=0, w_init=None, U_init=None, diag=False):
+    """SGLD with RMSprop step sizes (GPT_SGLD.jl:1121-1237).  Returns (w_store, U_store)
+    [, diag]; on the geodesic NaN bail-out prints the reference's message and returns zeros."""
+    phi = _f64(phi)
+    n, D, N = phi.shape
+    y = _f64(np.asarray(y, dtype=np.float64).ravel())
+    if y.size != N:
+        raise ValueError("phi and y disagree on N")
+    I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+    if I.shape != (Q, D):
+        raise ValueError("I must be (Q, D)")
+    cfg = make_config(n, D, N, r, Q, m, epsilon, epsilon, signal_var, 1.0, burnin, maxepoch,
+                      param_seed, True, True, 1, 0)
+    nb = -(-N // m)
+    T = maxepoch * nb
+    w_store = np.zeros((Q, T), order="F")
+    U_store = np.zeros((n, r, D, T), order="F")
+    dg = np.zeros((1 + D, (burnin + maxepoch) * nb), order="F") if diag else None
+    wi = _f64(w_init) if w_init is not None else None
+    Ui = _f64(U_init) if U_init is not None else None
+    code = lib().gpt_sgld_rmsprop(C.byref(cfg), float(epsilon), float(alpha), _ptr(phi), _ptr(y),
+                                  _ptr(I, P_I32), _ptr(wi) if wi is not None else None,
+                                  _ptr(Ui) if Ui is not None else None, _ptr(w_store),
+                                  _ptr(U_store), _ptr(dg) if diag else None)
+    if code == _lib.GPT_ERR_NAN_GEODESIC:
+        print("Get NaN when moving along Geodesic. Try smaller epsU")
+        w_store[:] = 0.0
+        U_store[:] = 0.0
+    else:
+        check(code)
+    return (w_store, U_store, dg) if diag else (w_store, U_store)
+
+
 def GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0, **kw):
     """Generation A/B sampler (GPT_SGLD_p.jl:146-243): ``sigma`` is the noise s.d. and the
     prior s.d. of w is sqrt(n^D/Q) (:155)."""

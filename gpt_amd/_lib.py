@@ -44,6 +44,9 @@ SIGNATURES = {
                                           C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), P_I32,
                                           C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]),
     "gpt_sgld_session_run": (C.c_int, [C.c_void_p, C.c_int64]),
+    "gpt_sgld_session_set_rmsprop": (C.c_int, [C.c_void_p, C.c_double, C.c_double]),
+    "gpt_sgld_rmsprop": (C.c_int, [C.POINTER(SGLDConfig), C.c_double, C.c_double, P_D, P_D, P_I32,
+                                   P_D, P_D, P_D, P_D, P_D]),
     "gpt_sgld_session_set_hyper": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_double,
                                              C.c_double, C.c_double]),
     "gpt_sgld_session_sync": (C.c_int, [C.c_void_p]),

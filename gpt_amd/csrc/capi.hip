@@ -257,6 +257,9 @@ extern "C" int gpt_device_count(void) {
 }
 
 static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t_local) {
+  if (P.rms)
+    return launch_step_rms(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
+                           t_local, s->stream);
   if (s->engine == kEngineChain)
     return launch_chain(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
                         t_local, s->stream);
@@ -342,6 +345,7 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     P.segpos = s->segpos.as<int32_t>();
   }
   P.stamps = nullptr;
+  P.rms = 0; P.rms_eps = 0.0; P.rms_alpha = 0.0;
   HIPCHK(s->tbase.alloc(sizeof(long long)));
   HIPCHK(hipMemset(s->tbase.p, 0, sizeof(long long)));
   HIPCHK(s->status.alloc(sizeof(int32_t) * nchains));
@@ -374,6 +378,7 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     C.diag = s->diag ? (double*)(base + b_w + b_U + b_temp + b_ord + b_ws + b_Us) : nullptr;
     C.status = s->status.as<int32_t>() + c;
     C.seed = seeds[c];
+    C.gw = C.gU = C.res = nullptr;
     C.epsw = cfg->epsw; C.epsU = cfg->epsU; C.signal_var = cfg->signal_var; C.sigma_w = cfg->sigma_w;
     host_init_state(n, r, D, Q, seeds[c], cfg->stiefel != 0, cfg->sigma_w, w0.data(), U0.data());
     host_epoch_orders(N, seeds[c], s->epochs, ord.data());
@@ -408,6 +413,38 @@ extern "C" int gpt_sgld_session_set_hyper(gpt_sgld_session* s, int32_t chain, do
   ChainDesc& C = s->chains_h[chain];
   C.epsw = epsw; C.epsU = epsU; C.signal_var = signal_var; C.sigma_w = sigma_w;
   HIPCHK(hipMemcpy(s->chains_d.as<ChainDesc>() + chain, &C, sizeof(ChainDesc), hipMemcpyHostToDevice));
+  return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_set_rmsprop(gpt_sgld_session* s, double epsilon, double alpha) {
+  if (!s) { set_error("null session"); return GPT_ERR_BAD_DIMS; }
+  if (s->engine != kEngineGrid) {
+    set_error("RMSprop steps run on the grid engine: create the session with store_flags bit 2");
+    return GPT_ERR_BAD_DIMS;
+  }
+  if (!s->cfg.stiefel || !s->cfg.langevin) {
+    set_error("GPT_SGLDERM_RMSprop is the SGLD + Stiefel sampler (langevin = stiefel = 1)");
+    return GPT_ERR_BAD_DIMS;
+  }
+  if (s->steps_done != 0 || s->gexec) { set_error("set RMSprop before the first run"); return GPT_ERR_BAD_DIMS; }
+  if (!(epsilon > 0) || !(alpha >= 0 && alpha < 1)) {
+    set_error("RMSprop needs epsilon > 0 and 0 <= alpha < 1"); return GPT_ERR_BAD_DIMS;
+  }
+  const StepParams& P = s->P;
+  const size_t bq = 8 * (size_t)P.Q, bu = 8 * (size_t)P.n * P.r * P.D, br = 8 * (size_t)P.m;
+  for (int c = 0; c < s->nchains; ++c) {
+    std::unique_ptr<DevMem> mem(new DevMem());
+    HIPCHK(mem->alloc(bq + bu + br));
+    HIPCHK(hipMemset(mem->p, 0, bq + bu + br));    // moving averages start at 0 (:1143-1144)
+    ChainDesc& C = s->chains_h[c];
+    C.gw = mem->as<double>();
+    C.gU = C.gw + P.Q;
+    C.res = C.gU + (size_t)P.n * P.r * P.D;
+    s->chain_mem.push_back(std::move(mem));
+  }
+  HIPCHK(hipMemcpy(s->chains_d.p, s->chains_h.data(), sizeof(ChainDesc) * s->nchains,
+                   hipMemcpyHostToDevice));
+  s->P.rms = 1; s->P.rms_eps = epsilon; s->P.rms_alpha = alpha;
   return GPT_OK;
 }
 
@@ -586,9 +623,12 @@ extern "C" int gpt_sgld_init(const gpt_sgld_config* cfg, double* w_out, double* 
   return GPT_OK;
 }
 
-extern "C" int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi, const double* y,
-                                   const int32_t* I, const double* w_init, const double* U_init,
-                                   double* w_store, double* U_store, double* diag) {
+// Shared driver of the host-pointer samplers: one chain, device copies of phi / y, the run, the
+// stores back (zero-filled + GPT_ERR_NAN_GEODESIC on the geodesic bail-out, GPT_SGLD.jl:422-424).
+static int host_sampler(const gpt_sgld_config* cfg, const double* phi, const double* y,
+                        const int32_t* I, const double* w_init, const double* U_init,
+                        double* w_store, double* U_store, double* diag, int extra_flags,
+                        double rms_eps, double rms_alpha) {
   if (!valid_cfg(cfg)) return GPT_ERR_BAD_DIMS;
   if (!phi || !y || !I) { set_error("null input"); return GPT_ERR_BAD_DIMS; }
   const size_t nphi = (size_t)cfg->n * cfg->D * cfg->N;
@@ -600,10 +640,14 @@ extern "C" int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi
   const double* pp = dphi.as<double>();
   const double* yy = dy.as<double>();
   gpt_sgld_session* s = nullptr;
-  const int flags = ((w_store || U_store) ? 1 : 0) | (diag ? 2 : 0);
+  const int flags = ((w_store || U_store) ? 1 : 0) | (diag ? 2 : 0) | extra_flags;
   int rc = gpt_sgld_session_create(cfg, 1, &cfg->seed, &pp, &yy, I, flags, nullptr, &s);
   if (rc != GPT_OK) return rc;
   std::unique_ptr<gpt_sgld_session, void (*)(gpt_sgld_session*)> guard(s, gpt_sgld_session_destroy);
+  if (rms_eps > 0) {
+    rc = gpt_sgld_session_set_rmsprop(s, rms_eps, rms_alpha);
+    if (rc != GPT_OK) return rc;
+  }
   if (w_init || U_init) {
     rc = session_set_state(s, 0, w_init, U_init);
     if (rc != GPT_OK) return rc;
@@ -618,6 +662,20 @@ extern "C" int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi
     return GPT_ERR_NAN_GEODESIC;
   }
   return GPT_OK;
+}
+
+extern "C" int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi, const double* y,
+                                   const int32_t* I, const double* w_init, const double* U_init,
+                                   double* w_store, double* U_store, double* diag) {
+  return host_sampler(cfg, phi, y, I, w_init, U_init, w_store, U_store, diag, 0, 0.0, 0.0);
+}
+
+extern "C" int gpt_sgld_rmsprop(const gpt_sgld_config* cfg, double epsilon, double alpha,
+                                const double* phi, const double* y, const int32_t* I,
+                                const double* w_init, const double* U_init, double* w_store,
+                                double* U_store, double* diag) {
+  if (!(epsilon > 0)) { set_error("RMSprop needs epsilon > 0"); return GPT_ERR_BAD_DIMS; }
+  return host_sampler(cfg, phi, y, I, w_init, U_init, w_store, U_store, diag, 4, epsilon, alpha);
 }
 
 extern "C" int gpt_samplenz(int64_t r, int64_t D, int64_t Q, uint64_t seed, int32_t* I_out) {

@@ -35,6 +35,9 @@ struct ChainDesc {
   int32_t* status;       // 0 ok, 1 NaN in geodesic
   uint64_t seed;
   double epsw, epsU, signal_var, sigma_w;   // per-chain hyper-parameters (sweeps)
+  double* gw;            // RMSprop (GPT_SGLD.jl:1121): Q moving average of squared gradw
+  double* gU;            //   n*r*D moving average of squared gradU
+  double* res;           //   m residuals of the step (written by the w phase)
 };
 
 struct StepParams {
@@ -47,8 +50,11 @@ struct StepParams {
   const int32_t* segpos;          // chain engine: pos (Q*D, rank of q in the (I[q,k], q) order of
                                   // dimension k, layout q + Q*k) then seg (D*(r+1) run starts)
   long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
+  int rms;                        // 1: GPT_SGLDERM_RMSprop steps (grid engine, two launches)
+  double rms_eps, rms_alpha;      // its epsilon and moving-average coefficient
 };
 constexpr int kStamps = 16;       // stamp slots per block
+constexpr double kRmsLambda = 1e-5;   // RMSprop smoothing (GPT_SGLD.jl:1146)
 
 GPT_HD size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
 
@@ -118,6 +124,9 @@ hipError_t launch_temp_init(const StepParams& P, const ChainDesc* chains, int nc
                             const long long* tbase, hipStream_t st);
 hipError_t launch_step(const StepParams& P, const ChainDesc* chains, int nchains,
                        const long long* tbase, int t_local, hipStream_t st);
+// RMSprop step = w phase (one workgroup per chain) then U phase (D workgroups per chain)
+hipError_t launch_step_rms(const StepParams& P, const ChainDesc* chains, int nchains,
+                           const long long* tbase, int t_local, hipStream_t st);
 hipError_t launch_advance(long long* tbase, long long by, hipStream_t st);
 bool rank_supported(int r);
 

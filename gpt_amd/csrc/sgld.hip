@@ -28,10 +28,10 @@ template <int R>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) void sgld_step_kernel(StepParams P,
                                                         const ChainDesc* __restrict__ chains,
                                                         const long long* __restrict__ tbase,
-                                                        int t_local) {
+                                                        int t_local, int kbase) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const ChainDesc C = chains[blockIdx.y];
-  const int k = blockIdx.x;
+  const int k = blockIdx.x + kbase;     // kbase = D: the RMSprop w phase (one workgroup)
   const int tid = threadIdx.x, wv = uni(tid >> 6);
   const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
@@ -70,7 +70,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     }
     for (int i = tid; i < MP; i += kNT) res_l[i] = 0.0;
     for (int o = tid; o < Q * D; o += kNT) IT_l[o] = gptr(P.I0)[o];   // I0 is already q + Q*k
-    const double* wsrc = C.w + (size_t)(t & 1) * Q;
+    // RMSprop U phase: A uses the new w written by the w phase (GPT_SGLD.jl:1193-1199)
+    const double* wsrc = C.w + (size_t)(((P.rms && k < D) ? t + 1 : t) & 1) * Q;
     for (int q = tid; q < Q; q += kNT) w_l[q] = gptr(wsrc)[q];
     for (int i = tid; i < Bt; i += kNT) {
       const int row = gptr(ord)[i];
@@ -108,6 +109,46 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   const long long post = t - P.burnin_steps;
   const bool store = post >= 0 && ((post + 1) % P.store_every) == 0;
   const long long slot = store ? (post + 1) / P.store_every - 1 : 0;
+
+  if (wblock && P.rms) {
+    // ---- RMSprop w phase (GPT_SGLD.jl:1182-1193): per-entry step sizes from the moving average
+    //      of squared per-sample gradients; the residuals go to the U phase (which sees new w)
+    for (int i = tid; i < Bt; i += kNT) gptr_w(C.res)[i] = res_l[i];
+    double gn2 = 0.0;
+    const double cR = 1.0 / ((double)Bt * C.signal_var);
+    for (int q = tid; q < Q; q += kNT) {
+      double g = 0.0;
+      for (int i0 = 0; i0 < Bt; i0 += 16) {
+        double vv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) vv[u] = 1.0;
+        for (int kk = 0; kk < D; ++kk) {
+          const double* row = temp_l + (kk * R + IT_l[kk * Q + q]) * MP + i0;
+#pragma unroll
+          for (int u = 0; u < 16; ++u) vv[u] *= row[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) g = fma(vv[u], res_l[i0 + u], g);
+      }
+      const double gr = g * cR;                                   // ĝw (:1182)
+      const double gwq = P.rms_alpha * gptr(C.gw)[q] + (1.0 - P.rms_alpha) * gr * gr;
+      gptr_w(C.gw)[q] = gwq;
+      const double ew = P.rms_eps / (sqrt(gwq) + kRmsLambda);     // :1186
+      const double wq = w_l[q];
+      const double gradw = (double)P.N * gr - wq;                 // :1190 (σ_w = 1)
+      const double wn = wq + ew * gradw / 2 +
+                        sqrt(ew) * normal_at(C.seed, (uint32_t)q, (uint32_t)t, kWNoise, 0);
+      gptr_w(C.w)[(size_t)((t + 1) & 1) * Q + q] = wn;
+      if (store && C.w_store) gptr_w(C.w_store)[(size_t)slot * Q + q] = wn;
+      gn2 = fma(gradw, gradw, gn2);
+    }
+    __syncthreads();
+    if (C.diag) {
+      const double tot = blk_sum(gn2, red);
+      if (tid == 0) C.diag[(size_t)t * (1 + D)] = sqrt(tot);
+    }
+    return;
+  }
 
   if (wblock) {
     // ---- gradw and the Langevin step on w (GPT_SGLD.jl:393, 411-414)
@@ -147,6 +188,10 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     return;
   }
 
+  if (P.rms) {   // the residuals are the w phase's (old w); V above used the new w for A only
+    for (int i = tid; i < Bt; i += kNT) res_l[i] = gptr(C.res)[i];
+    __syncthreads();
+  }
   // coef[l][i] = A[l][i]·res[i]; stage U^(k) (the union slot of temp_l is free now)
   for (int o = tid; o < R * Bt; o += kNT) {
     const int l = o / Bt, i = o - l * Bt;
@@ -164,7 +209,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   // ---- P2: gradU^(k) = (N/B)/σ² Σ_i phi[:,k,i] (A[:,k,i] res_i)ᵀ   (GPT_SGLD.jl:396-408)
   const double cU = cN / C.signal_var;
   const double sq = sqrt(C.epsU);
-  double gn2 = 0.0;
+  double gn2 = 0.0, esum = 0.0;
   // Uniform trip count (j clamped, writes masked): every lane takes part in the row-vector
   // load below, so v_readlane never reads a lane that skipped it.
   for (int j0 = 0; j0 < n; j0 += kNT) {
@@ -202,7 +247,19 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
 #pragma unroll
         for (int l = 0; l < R; ++l) acc[l] = fma(p[u], coef_l[l * MP + i0 + u], acc[l]);
     }
-    if (jok) {
+    if (jok && P.rms) {           // :1212-1227: ĝU, moving average, N·ĝU kept until εU_k is known
+#pragma unroll
+      for (int l = 0; l < R; ++l) {
+        const double gr = acc[l] / ((double)Bt * C.signal_var);
+        const size_t e = (size_t)n * R * k + (size_t)n * l + j;
+        const double gu = P.rms_alpha * gptr(C.gU)[e] + (1.0 - P.rms_alpha) * gr * gr;
+        gptr_w(C.gU)[e] = gu;
+        esum += P.rms_eps / (sqrt(gu) + kRmsLambda);
+        const double G = (double)P.N * gr;
+        gn2 = fma(G, G, gn2);
+        W_l[l * NS + j] = G;
+      }
+    } else if (jok) {
 #pragma unroll
       for (int l = 0; l < R; ++l) {
         const double G = acc[l] * cU;
@@ -219,6 +276,21 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   if (C.diag) {
     const double tot = blk_sum(gn2, red);
     if (tid == 0) C.diag[(size_t)t * (1 + D) + 1 + k] = sqrt(tot);
+  }
+  double sk = sq;                 // geodesic time: √εU, or √mean(εU_k) under RMSprop (:1218)
+  if (P.rms) {
+    __syncthreads();
+    sk = sqrt(blk_sum(esum, red) / ((double)n * R));
+    constexpr int RE = R + (R & 1);
+    for (int j = tid; j < n; j += kNT) {       // drive √εU_k·gradU/2 + ξ (:1231)
+#pragma unroll
+      for (int l = 0; l < R; l += 2) {
+        double z0, z1;
+        normal_pair(C.seed, (uint32_t)((l + RE * j) >> 1), (uint32_t)t, kUNoise, (uint32_t)k, z0, z1);
+        W_l[l * NS + j] = sk * W_l[l * NS + j] / 2 + z0;
+        if (l + 1 < R) W_l[(l + 1) * NS + j] = sk * W_l[(l + 1) * NS + j] / 2 + z1;
+      }
+    }
   }
   __syncthreads();
   STAMP(4);
@@ -248,7 +320,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     // ---- geod (GPT_SGLD.jl:19-37): A = Uᵀmom, S = momᵀmom
     blk_gram<R>(U_l, W_l, NS, n, 1, Ag, red);      // Ag = Uᵀmom and Sg = momᵀmom in one pass
     STAMP(6);
-    const double tt = sq;
+    const double tt = sk;
     const int nn = 2 * R;
     double* X0 = (double*)(smem + L.o_x0);     // U_l / red are dead from here to the update
     double* X1 = (double*)(smem + L.o_x1);
@@ -409,7 +481,25 @@ hipError_t launch_step(const StepParams& P, const ChainDesc* chains, int nchains
 #define CASE(RR)                                                                              \
   case RR:                                                                                    \
     hipLaunchKernelGGL(sgld_step_kernel<RR>, grid, dim3(kNT), L.bytes, st, P, chains, tbase,  \
-                       t_local);                                                              \
+                       t_local, 0);                                                           \
+    break;
+    GPT_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_step_rms(const StepParams& P, const ChainDesc* chains, int nchains,
+                           const long long* tbase, int t_local, hipStream_t st) {
+  const StepLayout L = step_layout(P.n, P.D, P.r, P.Q, P.m);
+  switch (P.r) {
+#define CASE(RR)                                                                              \
+  case RR:                                                                                    \
+    hipLaunchKernelGGL(sgld_step_kernel<RR>, dim3(1, nchains), dim3(kNT), L.bytes, st, P,     \
+                       chains, tbase, t_local, P.D);                                          \
+    hipLaunchKernelGGL(sgld_step_kernel<RR>, dim3(P.D, nchains), dim3(kNT), L.bytes, st, P,   \
+                       chains, tbase, t_local, 0);                                            \
     break;
     GPT_RANKS(CASE)
 #undef CASE

@@ -67,6 +67,10 @@ class SGLDSession:
         check(lib().gpt_sgld_session_set_hyper(self._h, chain, float(epsw), float(epsU),
                                                float(signal_var), float(sigma_w)))
 
+    def set_rmsprop(self, epsilon, alpha):
+        """Switch this (grid-engine) session to GPT_SGLDERM_RMSprop steps (GPT_SGLD.jl:1121)."""
+        check(lib().gpt_sgld_session_set_rmsprop(self._h, float(epsilon), float(alpha)))
+
     def run(self, nsteps):
         check(lib().gpt_sgld_session_run(self._h, int(nsteps)))
 

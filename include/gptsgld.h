@@ -84,6 +84,14 @@ int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi, const dou
                         const int32_t* I, const double* w_init, const double* U_init,
                         double* w_store, double* U_store, double* diag);
 
+/* GPT_SGLDERM_RMSprop(phi,y,signal_var,I,r,Q,m,epsilon,alpha,burnin,maxepoch)
+ * GPT_SGLD.jl:1121-1237: per-entry RMSprop step sizes for w, one averaged step per U^(k), w
+ * updated before A.  cfg's epsw/epsU/sigma_w are not used (sigma_w = 1 as in the reference);
+ * cfg->langevin and cfg->stiefel must be 1.  Runs on the grid engine. */
+int gpt_sgld_rmsprop(const gpt_sgld_config* cfg, double epsilon, double alpha, const double* phi,
+                     const double* y, const int32_t* I, const double* w_init,
+                     const double* U_init, double* w_store, double* U_store, double* diag);
+
 /* Multi-chain, device-resident session (benchmark / multi-GPU path).  Chains share the
  * config except seed; chain c reads phi_dev[c], y_dev[c] (device pointers; may alias). */
 typedef struct gpt_sgld_session gpt_sgld_session;
@@ -97,6 +105,9 @@ int gpt_sgld_session_set_hyper(gpt_sgld_session* s, int32_t chain, double epsw, 
                                double signal_var, double sigma_w);
 /* Queue `nsteps` SGLD steps of every chain on the session stream (asynchronous). */
 int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps);
+/* Switch a grid-engine session (store_flags bit 2) to GPT_SGLDERM_RMSprop steps; call before
+ * the first run. */
+int gpt_sgld_session_set_rmsprop(gpt_sgld_session* s, double epsilon, double alpha);
 int gpt_sgld_session_sync(gpt_sgld_session* s);
 /* Device pointers of chain c's current state and stores (for pred / collectives). */
 int gpt_sgld_session_state(gpt_sgld_session* s, int32_t chain, double** w_dev, double** U_dev,

@@ -9,7 +9,7 @@
 module GPT_SGLD_HIP
 
 export datawhitening, feature, featureNotensor, samplenz, GPTregression, GPT_SGLDERM, pred, RMSE,
-       GPNT_SGLD
+       GPNT_SGLD, GPT_SGLDERM_RMSprop
 
 const LIB = get(ENV, "GPTSGLD_LIB", joinpath(@__DIR__, "..", "gpt_amd", "libgptsgld.so"))
 
@@ -106,6 +106,26 @@ function GPT_SGLDERM(phi::Array{Float64,3}, y::Array{Float64}, sigma::Real, I::A
     n, D, _ = size(phi)
     return GPTregression(phi, y, sigma^2, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed;
                          sigma_w=sqrt(Float64(n)^D / Q))
+end
+
+# GPT_SGLDERM_RMSprop(phi,y,signal_var,I,r,Q,m,epsilon,alpha,burnin,maxepoch)  GPT_SGLD.jl:1121
+function GPT_SGLDERM_RMSprop(phi::Array{Float64,3}, y::Array{Float64}, signal_var::Real,
+                             I::Array{Int32,2}, r::Integer, Q::Integer, m::Integer, epsilon::Real,
+                             alpha::Real, burnin::Integer, maxepoch::Integer, param_seed::Integer=0)
+    n, D, N = size(phi)
+    T = maxepoch * cld(N, m)
+    cfg = Ref(SGLDConfig(n, D, N, r, Q, m, epsilon, epsilon, signal_var, 1.0, burnin, maxepoch,
+                         UInt64(param_seed), Int32(1), Int32(1), 1, 0))
+    w_store = zeros(Q, T); U_store = zeros(n, r, D, T)
+    rc = ccall((:gpt_sgld_rmsprop, LIB), Cint,
+               (Ref{SGLDConfig}, Float64, Float64, Ptr{Float64}, Ptr{Float64}, Ptr{Int32},
+                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+               cfg, epsilon, alpha, phi, vec(y), I, C_NULL, C_NULL, w_store, U_store, C_NULL)
+    if rc == 1
+        return zeros(Q, T), zeros(n, r, D, T)
+    end
+    check(rc)
+    return w_store, U_store
 end
 
 # pred(w,U,I,phitest)  GPT_SGLD.jl:233

@@ -378,6 +378,83 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
     return w_store, U_store, info
 
 
+RMS_LAMBDA = 1e-5   # GPT_SGLD.jl:1146 smoothing constant
+
+
+def GPT_SGLDERM_RMSprop(phi, y, signal_var, I, r, Q, m, epsilon, alpha, burnin, maxepoch,
+                        param_seed=0, w_init=None, U_init=None, max_steps=None, record=False):
+    """GPT_SGLD.jl:1121-1237 — SGLD with RMSprop-preconditioned step sizes (σ_w = 1).
+
+    Differences from GPTregression, all as in the reference: the moving averages
+    gw = α·gw + (1-α)·ĝw², gU = α·gU + (1-α)·ĝU² of the squared *per-sample mean* gradients
+    (ĝw = V·res/(B·σ²) :1182, ĝU = Ψ_k·res/(B·σ²) :1212); per-entry step sizes
+    εw = ε/(√gw + λ) (:1186) and one scalar step per dimension εU_k = mean(ε/(√gU_k + λ)) (:1218);
+    **w is updated before computeA** (:1193 vs :1199), so A (and gradU) use the new w.
+    Noise streams and permutations follow the framework contract of GPTregression.
+    """
+    phi = np.asarray(phi, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64).ravel()
+    n, D, N = phi.shape
+    numbatches = -(-N // m)
+    if w_init is None or U_init is None:
+        w0, U0 = init_state(n, r, D, Q, param_seed, True, 1.0)
+    w = np.array(w0 if w_init is None else w_init, dtype=np.float64)
+    U = np.array(U0 if U_init is None else U_init, dtype=np.float64, order="F")
+    nstore = maxepoch * numbatches
+    w_store = np.zeros((Q, nstore), order="F")
+    U_store = np.zeros((n, r, D, nstore), order="F")
+    gw = np.zeros(Q)
+    gU = np.zeros((n, r, D), order="F")
+    info = dict(status=0, gradw_norm=[], gradU_norm=[])
+    order = np.arange(N)
+    step = 0
+    for epoch in range(1, burnin + maxepoch + 1):
+        order = order[px.randperm(N, param_seed, epoch - 1)]
+        for batch in range(1, numbatches + 1):
+            if max_steps is not None and step >= max_steps:
+                return w_store, U_store, info
+            idx = order[m * (batch - 1): min(m * batch, N)]
+            phi_b = phi[:, :, idx]
+            y_b = y[idx]
+            B = len(idx)
+            temp = phidotU(U, phi_b)
+            V = computeV(temp, I)
+            fhat = computefhat(V, w)
+            res = y_b - fhat
+            gradw = (1.0 / B) * (V @ res) / signal_var                       # :1182
+            gw = alpha * gw + (1 - alpha) * gradw ** 2                          # :1185
+            epsw = epsilon / (np.sqrt(gw) + RMS_LAMBDA)                         # :1186
+            gradw = N * gradw - w                                               # :1190 (σ_w = 1)
+            w = w + epsw * gradw / 2 + np.sqrt(epsw) * px.normals(Q, param_seed, step, px.W_NOISE, 0)
+            U_phi = computeU_phi(V, temp, I)
+            A = computeA(U_phi, w, I, r)                                        # new w (:1199)
+            Psi = computePsi(A, phi_b)
+            gradU = np.empty((n, r, D), order="F")
+            for k in range(D):
+                gradU[:, :, k] = ((1.0 / B) * (Psi[:, :, k] @ res) / signal_var).reshape((n, r), order="F")
+            gU = alpha * gU + (1 - alpha) * gradU ** 2                          # :1216
+            epsU = epsilon / (np.sqrt(gU) + RMS_LAMBDA)                         # :1217
+            meanepsU = epsU.mean(axis=(0, 1))                                   # :1218
+            gradU = gradU * N                                                   # :1227
+            if record:
+                info["gradw_norm"].append(np.linalg.norm(gradw))
+                info["gradU_norm"].append([np.linalg.norm(gradU[:, :, k]) for k in range(D)])
+            for k in range(D):
+                sk = math.sqrt(meanepsU[k])
+                mom = proj(U[:, :, k], sk * gradU[:, :, k] / 2 + u_noise(n, r, param_seed, step, k))
+                Un, ok = geod(U[:, :, k], mom, sk)
+                if not ok:
+                    info["status"] = 1
+                    return np.zeros_like(w_store), np.zeros_like(U_store), info
+                U[:, :, k] = Un
+            if epoch > burnin:
+                s = (epoch - burnin - 1) * numbatches + (batch - 1)
+                w_store[:, s] = w
+                U_store[:, :, :, s] = U
+            step += 1
+    return w_store, U_store, info
+
+
 def GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0, **kw):
     """GPT_SGLD_p.jl:146-243 (Generations A/B): ``sigma`` is the noise s.d. and
     σ_w = sqrt(n^D/Q) (:155).  Follows GPTregression's batch labels (the ``y[batch]`` slip

@@ -145,6 +145,34 @@ def test_sampler_trajectory_matches_oracle(name, engine):
                 assert np.abs(Uk.T @ Uk - np.eye(r)).max() < 1e-10
 
 
+RMS_CASES = {
+    # name: (n, D, N, r, Q, m, burnin, maxepoch, epsilon)
+    "small": (16, 3, 40, 2, 6, 8, 1, 2, 1e-5),
+    "ragged": (24, 4, 37, 3, 10, 8, 0, 3, 1e-5),
+    # At ε = 1e-5 this shape is ill-conditioned in the oracle itself: a 1e-15 relative
+    # perturbation of U_init grows to 8e-8 in three steps (one RMSprop geodesic step of
+    # t = √mean(εU) ≈ 0.06 over momenta of norm ≈ 20).  ε = 1e-6 keeps it at 2e-12.
+    "kin40k_shape": (500, 8, 150, 5, 200, 50, 0, 1, 1e-6),
+}
+
+
+@pytest.mark.parametrize("name", list(RMS_CASES))
+def test_rmsprop_trajectory_matches_oracle(name):
+    """GPT_SGLDERM_RMSprop (GPT_SGLD.jl:1121-1237) against the oracle restatement."""
+    n, D, N, r, Q, m, burnin, maxepoch, eps = RMS_CASES[name]
+    p = make_problem(n, D, N, r, Q, seed=13)
+    alpha, sv, seed = 0.9, 0.05, 29
+    ws, Us, dg = G().GPT_SGLDERM_RMSprop(p["phi"], p["y"], sv, p["I"], r, Q, m, eps, alpha, burnin,
+                                         maxepoch, seed, diag=True)
+    wo, Uo, info = R.GPT_SGLDERM_RMSprop(p["phi"], p["y"], sv, p["I"], r, Q, m, eps, alpha, burnin,
+                                         maxepoch, seed, record=True)
+    assert info["status"] == 0
+    assert rel(ws, wo) < 1e-8, rel(ws, wo)
+    assert rel(Us, Uo) < 1e-8, rel(Us, Uo)
+    assert rel(dg[0], np.array(info["gradw_norm"])) < 1e-9
+    assert rel(dg[1:], np.array(info["gradU_norm"]).T) < 1e-9
+
+
 def test_sgldERM_generation_a_mapping():
     n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
     p = make_problem(n, D, N, r, Q, seed=4)

@@ -130,3 +130,32 @@ def test_reference_curves_fixture():
     assert abs(c["testRMSE_kin40k"][-1] - 0.2385) < 1e-3
     assert abs(c["testRMSE_kin40k"][-50:].mean() - 0.2448) < 2e-3 or c["testRMSE_kin40k"][-50:].mean() > 0.2
     assert abs(c["testRMSE_PP"][-1] - 4.1446) < 1e-3
+
+
+def test_rmsprop_oracle_first_step_and_invariants():
+    """GPT_SGLDERM_RMSprop (GPT_SGLD.jl:1121-1237): the first w update restated by hand from the
+    shared gradient pieces, Stiefel invariance of every stored U."""
+    import math
+    from oracle import philox as px
+    rng = np.random.default_rng(5)
+    n, D, N, r, Q, m = 10, 3, 30, 2, 6, 10
+    X = rng.standard_normal((N, D)); Z = rng.standard_normal((n, D)); b = 2 * np.pi * rng.random((n, D))
+    phi = R.feature(X, np.ones(D), 1.0, 2.0, Z, b)
+    I = R.samplenz(r, D, Q, 4)
+    y = rng.standard_normal(N)
+    eps, alpha, sv, seed = 1e-3, 0.9, 0.2, 7
+    ws, Us, info = R.GPT_SGLDERM_RMSprop(phi, y, sv, I, r, Q, m, eps, alpha, 0, 2, seed)
+    assert info["status"] == 0
+    w0, U0 = R.init_state(n, r, D, Q, seed)
+    idx = px.randperm(N, seed, 0)[:m]
+    temp = R.phidotU(U0, phi[:, :, idx])
+    V = R.computeV(temp, I)
+    res = y[idx] - V.T @ w0
+    gr = V @ res / (m * sv)
+    gw = (1 - alpha) * gr ** 2
+    ew = eps / (np.sqrt(gw) + R.RMS_LAMBDA)
+    w1 = w0 + ew * (N * gr - w0) / 2 + np.sqrt(ew) * px.normals(Q, seed, 0, px.W_NOISE, 0)
+    assert np.allclose(ws[:, 0], w1, rtol=1e-13, atol=1e-13)
+    for s in range(Us.shape[3]):
+        for k in range(D):
+            assert np.abs(Us[:, :, k, s].T @ Us[:, :, k, s] - np.eye(r)).max() < 1e-10
