@@ -14,6 +14,7 @@ GPT_ERR_NAN_GEODESIC = 1
 GPT_ERR_BAD_DIMS = 2
 GPT_ERR_HIP = 3
 GPT_ERR_NAN_THETA = 4
+GPT_ERR_NOT_SPD = 5
 
 P_D = C.POINTER(C.c_double)
 P_I32 = C.POINTER(C.c_int32)
@@ -71,6 +72,9 @@ SIGNATURES = {
                                 C.c_int64, C.c_int64, C.c_int64, C.c_double, P_D, P_D]),
     "gpt_gpnt_sgld": (C.c_int, [P_D, P_D, C.c_int64, C.c_int64, C.c_double, C.c_double, C.c_int64,
                                 C.c_double, C.c_double, C.c_int64, C.c_int64, C.c_uint64, P_D]),
+    "gpt_tgp_gibbs": (C.c_int, [P_D, P_D, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                C.c_double, C.c_int64, C.c_int64, C.c_uint64, P_I32, P_D, P_D,
+                                P_I32]),
     "gpt_last_error": (C.c_char_p, []),
     "gpt_sgld_lds_bytes": (C.c_int64, [C.c_int64] * 5),
     "gpt_device_count": (C.c_int, []),

@@ -899,3 +899,57 @@ extern "C" int gpt_gpnt_sgld(const double* phi, const double* y, int64_t n, int6
   HIPCHK(hipMemcpy(theta_store, dst.p, 8 * (size_t)n * total, hipMemcpyDeviceToHost));
   return GPT_OK;
 }
+
+extern "C" int gpt_tgp_gibbs(const double* b, const double* y, int64_t n, int64_t D, int64_t N,
+                             int64_t r, int64_t q, double sigma, int64_t num_iterations,
+                             int64_t burnin, uint64_t seed, const int32_t* I, double* W_out,
+                             double* U_out, int32_t* I_out) {
+  if (!b || !y || !W_out || !U_out || n < 1 || D < 1 || N < 1 || q < 1 || burnin < 0 ||
+      num_iterations <= burnin || !(sigma > 0)) {
+    set_error("bad GPT_inf arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  if (!rank_supported((int)r)) { set_error("rank r not instantiated (supported: 1-6,8,10,12,15,16,20)"); return GPT_ERR_BAD_DIMS; }
+  if (n * r > 8192 || q > 8192 || (double)n * D * N > 2e9) { set_error("dimension too large"); return GPT_ERR_BAD_DIMS; }
+  std::vector<int32_t> I0((size_t)q * D);
+  for (int64_t e = 0; e < q * D; ++e) {
+    int32_t v;
+    if (I) {
+      v = I[e];
+      if (v < 1 || v > r) { set_error("I entries must be in 1..r"); return GPT_ERR_BAD_DIMS; }
+    } else {
+      const U4 x = philox4x32((uint32_t)e, 0, kTgpI, 0, seed);
+      v = 1 + (int32_t)(((uint64_t)x.x * (uint64_t)r) >> 32);
+    }
+    if (I_out) I_out[e] = v;
+    I0[e] = v - 1;
+  }
+  const int64_t nr = n * r, T = num_iterations - burnin;
+  std::vector<double> U0((size_t)nr * D);
+  const double su = std::sqrt(1.0 / (double)r);
+  for (int64_t d = 0; d < D; ++d)
+    for (int64_t e = 0; e < nr; ++e) U0[d * nr + e] = su * host_normal(seed, (uint32_t)e, 0, kTgpUInit, (uint32_t)d);
+  DevMem db, dy, dI, dU, dW, dUh, dst;
+  HIPCHK(db.alloc(8 * (size_t)n * D * N));
+  HIPCHK(dy.alloc(8 * (size_t)N));
+  HIPCHK(dI.alloc(4 * I0.size()));
+  HIPCHK(dU.alloc(8 * U0.size()));
+  HIPCHK(dW.alloc(8 * (size_t)q * T));
+  HIPCHK(dUh.alloc(8 * (size_t)nr * D * T));
+  HIPCHK(dst.alloc(4));
+  HIPCHK(hipMemcpy(db.p, b, 8 * (size_t)n * D * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy.p, y, 8 * (size_t)N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dI.p, I0.data(), 4 * I0.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dU.p, U0.data(), 8 * U0.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(dst.p, 0, 4));
+  hipError_t e = tgp_gibbs(db.as<double>(), dy.as<double>(), (int)n, (int)D, N, (int)r, (int)q, sigma,
+                           (int)num_iterations, (int)burnin, seed, dI.as<int32_t>(), dU.as<double>(),
+                           dW.as<double>(), dUh.as<double>(), dst.as<int32_t>(), nullptr);
+  if (e != hipSuccess) return hip_fail(e, "tgp gibbs");
+  HIPCHK(hipStreamSynchronize(nullptr));
+  int32_t stt = 0;
+  HIPCHK(hipMemcpy(&stt, dst.p, 4, hipMemcpyDeviceToHost));
+  if (stt) { set_error("PosDefException: Gibbs precision matrix not positive definite"); return GPT_ERR_NOT_SPD; }
+  HIPCHK(hipMemcpy(W_out, dW.p, 8 * (size_t)q * T, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(U_out, dUh.p, 8 * (size_t)nr * D * T, hipMemcpyDeviceToHost));
+  return GPT_OK;
+}

@@ -147,6 +147,9 @@ hipError_t launch_feature(const double* X, long long N, int D, const double* ls,
 hipError_t launch_feature_notensor(const double* X, long long N, int D, const double* ls,
                                    double c, const double* Z, const double* b, int n,
                                    double* phi, hipStream_t st);
+hipError_t tgp_gibbs(const double* b, const double* y, int n, int D, long long N, int r, int q,
+                     double sigma, int iters, int burnin, uint64_t seed, const int32_t* I0,
+                     double* U, double* W_hist, double* U_hist, int32_t* status, hipStream_t st);
 hipError_t launch_gpnt(const double* phi, const double* y, const int32_t* order, int n, int N,
                        int m, int nb, long long total, double signal_var, double sigma_theta,
                        double eps_theta, double decay_rate, uint64_t seed, double* theta,

@@ -30,6 +30,7 @@ extern "C" {
 #define GPT_ERR_BAD_DIMS 2
 #define GPT_ERR_HIP 3
 #define GPT_ERR_NAN_THETA 4
+#define GPT_ERR_NOT_SPD 5      /* a Gibbs precision matrix failed Cholesky (PosDefException) */
 
 /* Sampler configuration: the scalar arguments of GPTregression (GPT_SGLD.jl:345) plus the
  * framework's store policy.  sigma_w = 1 is Generation C/D (GPT_SGLD.jl:354); Generation A/B
@@ -152,6 +153,18 @@ int gpt_pred_mean(const double* w_store, const double* U_store, const int32_t* I
 int gpt_gpnt_sgld(const double* phi, const double* y, int64_t n, int64_t N, double signal_var,
                   double sigma_theta, int64_t m, double eps_theta, double decay_rate,
                   int64_t burnin, int64_t maxepoch, uint64_t seed, double* theta_store);
+
+/* ---- tensor-GP Gibbs sampler (§8 a25) ----------------------------------------------- */
+/* GPT_inf(b,y,sigma,n,r,q,num_iterations,burnin) TGP.jl:37-86 on whitened data.
+ * b (n, D, N) column-major feature array (TGP.feature, TGP.jl:6-14), y (N).
+ * I (q, D) 1-based core indices; NULL draws them (TGP.jl:50) on the TGP_I Philox stream, and
+ * I_out (optional) receives the indices used.  U starts at sqrt(1/r)·randn (TGP.jl:48-49,
+ * TGP_U_INIT stream).  W_out (q, T), U_out (n, r, D, T), T = num_iterations - burnin: the W
+ * draw of each kept sweep and the U it was drawn against (TGP.jl:60-63).
+ * Returns GPT_ERR_NOT_SPD when a precision matrix is not positive definite. */
+int gpt_tgp_gibbs(const double* b, const double* y, int64_t n, int64_t D, int64_t N, int64_t r,
+                  int64_t q, double sigma, int64_t num_iterations, int64_t burnin, uint64_t seed,
+                  const int32_t* I, double* W_out, double* U_out, int32_t* I_out);
 
 const char* gpt_last_error(void);
 /* LDS bytes one step workgroup needs for this shape (must be <= 163840). */

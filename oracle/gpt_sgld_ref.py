@@ -509,3 +509,81 @@ def posterior_mean_pred(w_store, U_store, I, phitest, cols=None):
         acc = p if acc is None else acc + p
         cnt += 1
     return acc / cnt
+
+
+# --------------------------------------------------------------------------- TGP Gibbs (a25)
+def tgp_draw_I(q, D, r, seed):
+    """TGP.jl:50 ``I = rand(DiscreteUniform(1, r), q, D)`` on the TGP_I stream: entry e = i + q·d
+    is 1 + floor(x0·r / 2^32) of Philox block e (with replacement, unlike samplenz)."""
+    x0, _, _, _ = px.philox4x32(np.arange(q * D, dtype=np.uint32), 0, px.TGP_I, 0, seed)
+    return (1 + ((x0.astype(np.uint64) * np.uint64(r)) >> np.uint64(32))).astype(np.int32).reshape(
+        (q, D), order="F")
+
+
+def tgp_init_U(n, r, D, seed):
+    """TGP.jl:48-49: U_d = sqrt(1/r)·randn(n, r) (TGP_U_INIT stream, tag d)."""
+    U = np.empty((n, r, D), order="F")
+    for d in range(D):
+        U[:, :, d] = math.sqrt(1.0 / r) * px.normals(n * r, seed, 0, px.TGP_U_INIT, d).reshape(
+            (n, r), order="F")
+    return U
+
+
+def tgp_V(U, I, b):
+    """TGP.jl:55: V[i,j] = Π_d U_d[:, I[i,d]]ᵀ b[:, d, j]  (q × N)."""
+    return computeV(phidotU(U, b), I)
+
+
+def GPT_inf(b, y, sigma, n, r, q, num_iterations, burnin, seed, I=None):
+    """TGP.jl:37-86 (Gibbs sweep of the tensor GP) on whitened data: ``b`` (n, D, N) is the
+    feature array of TGP.feature (TGP.jl:6-14) and ``y`` (N) the whitened targets.
+
+    Per sweep: W ~ N(Mu_w, invSigma_w⁻¹) through the upper Cholesky factor (:57-59); for each k
+    the leave-one-out C (r × N, run sums over I[:,k]), Ck = C ⊗ b_k, invSigma_U = CkCkᵀ/σ² + r·I,
+    U_k = invSigma_U⁻¹ z + Mu_U (:76-79 — ``factorize(invSigma_U) \ randn`` solves, as in the
+    reference) and V refreshed with the new U_k (:81).  Runs C[l,:] of values l absent from
+    I[:,k] are uninitialised in the reference (Array(Float64,r,N)); here they are 0.
+    Returns (W_array (q, T), V_array (n, r, D, T), I), T = num_iterations - burnin."""
+    from scipy.linalg import solve_triangular
+    b = np.asarray(b, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64).ravel()
+    _, D, N = b.shape
+    sigma_u = math.sqrt(1.0 / r)
+    sigma_w = math.sqrt(float(r) ** D / q)
+    U = tgp_init_U(n, r, D, seed)
+    if I is None:
+        I = tgp_draw_I(q, D, r, seed)
+    T = num_iterations - burnin
+    W_array = np.zeros((q, T), order="F")
+    V_array = np.zeros((n, r, D, T), order="F")
+    s2 = sigma ** 2
+    for it in range(1, num_iterations + 1):
+        temp = phidotU(U, b)
+        V = computeV(temp, I)
+        inv_w = V @ V.T / s2 + np.eye(q) / sigma_w ** 2
+        L = np.linalg.cholesky(inv_w)
+        mu = solve_triangular(L.T, solve_triangular(L, V @ y / s2, lower=True), lower=False)
+        z = px.normals(q, seed, it - 1, px.TGP_W_NOISE, 0)
+        W = solve_triangular(L.T, z, lower=False) + mu                         # chol(·,:U) \ z
+        if it > burnin:
+            W_array[:, it - burnin - 1] = W
+            V_array[:, :, :, it - burnin - 1] = U
+        for k in range(D):
+            tk = temp[k, I[:, k] - 1, :]                                        # (q, N)
+            Vk = V / tk
+            Vkk = W[:, None] * Vk
+            C = np.zeros((r, N))
+            for l in range(1, r + 1):
+                sel = I[:, k] == l
+                if sel.any():
+                    C[l - 1, :] = Vkk[sel, :].sum(axis=0)
+            Ck = (C[:, None, :] * b[None, :, k, :]).reshape((r * n, N))          # row (l, j) -> l·n + j
+            inv_u = Ck @ Ck.T / s2 + np.eye(n * r) / sigma_u ** 2
+            Lu = np.linalg.cholesky(inv_u)
+            rhs = Ck @ y / s2
+            zu = px.normals(n * r, seed, it - 1, px.TGP_U_NOISE, k)
+            x = solve_triangular(Lu.T, solve_triangular(Lu, rhs + zu, lower=True), lower=False)
+            U[:, :, k] = x.reshape((n, r), order="F")
+            temp[k] = U[:, :, k].T @ b[:, k, :]
+            V = Vk * temp[k, I[:, k] - 1, :]
+    return W_array, V_array, I

@@ -36,6 +36,8 @@ W1 = np.uint32(0xBB67AE85)
 MASK32 = np.uint64(0xFFFFFFFF)
 
 W_INIT, U_INIT, PERM, W_NOISE, U_NOISE, THETA_INIT, THETA_NOISE = 1, 2, 3, 4, 5, 6, 7
+# TGP Gibbs (TGP.jl:37-86): U init, the core index draw, and the two Gaussian draws per sweep
+TGP_U_INIT, TGP_I, TGP_W_NOISE, TGP_U_NOISE = 11, 12, 13, 14
 
 
 def philox4x32(c0, c1, c2, c3, seed):

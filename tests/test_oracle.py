@@ -159,3 +159,71 @@ def test_rmsprop_oracle_first_step_and_invariants():
     for s in range(Us.shape[3]):
         for k in range(D):
             assert np.abs(Us[:, :, k, s].T @ Us[:, :, k, s] - np.eye(r)).max() < 1e-10
+
+
+def _gibbs_literal(b, y, sigma, n, r, q, iters, burnin, seed, I):
+    """TGP.jl:37-86 written as the reference's element-wise comprehensions (tiny sizes only),
+    with the same Philox draws and the same zero-initialised absent runs as the oracle."""
+    _, D, N = b.shape
+    su2, sw2 = 1.0 / r, float(r) ** D / q
+    U = R.tgp_init_U(n, r, D, seed)
+    dot = lambda k, l, j: sum(U[a, l - 1, k] * b[a, k, j] for a in range(n))     # noqa: E731
+    Ws, Us = [], []
+    for it in range(1, iters + 1):
+        V = np.array([[math.prod(dot(d, I[i, d], j) for d in range(D)) for j in range(N)]
+                      for i in range(q)])
+        M = V @ V.T / sigma ** 2 + np.eye(q) / sw2
+        mu = np.linalg.solve(M, V @ y / sigma ** 2)
+        Lt = np.linalg.cholesky(M).T                                          # chol(M, :U)
+        W = np.linalg.solve(Lt, px.normals(q, seed, it - 1, px.TGP_W_NOISE, 0)) + mu
+        if it > burnin:
+            Ws.append(W.copy()); Us.append(U.copy())
+        for k in range(D):
+            Vk = np.array([[V[l, j] / dot(k, I[l, k], j) for j in range(N)] for l in range(q)])
+            Vkk = W[:, None] * Vk
+            C = np.zeros((r, N))
+            for l in set(I[:, k]):
+                C[l - 1, :] = Vkk[I[:, k] == l, :].sum(axis=0)
+            Ck = np.array([[C[row // n, j] * b[row % n, k, j] for j in range(N)]
+                           for row in range(n * r)])                          # repeat ⊙ repmat
+            Mu = Ck @ Ck.T / sigma ** 2 + np.eye(n * r) / su2
+            z = px.normals(n * r, seed, it - 1, px.TGP_U_NOISE, k)
+            x = np.linalg.solve(Mu, z) + np.linalg.solve(Mu, Ck @ y / sigma ** 2)
+            U[:, :, k] = x.reshape((n, r), order="F")
+            V = np.array([[Vk[l, j] * dot(k, I[l, k], j) for j in range(N)] for l in range(q)])
+    return np.array(Ws).T, np.moveaxis(np.array(Us), 0, -1)
+
+
+def test_tgp_gibbs_oracle_matches_literal_restatement():
+    """The vectorised GPT_inf restatement against TGP.jl's comprehension form (tiny sizes)."""
+    rng = np.random.default_rng(5)
+    n, D, N, r, q, sigma = 4, 3, 9, 2, 5, 0.4
+    b = rng.standard_normal((n, D, N))
+    y = rng.standard_normal(N)
+    I = R.tgp_draw_I(q, D, r, 11)
+    W, U, I2 = R.GPT_inf(b, y, sigma, n, r, q, 3, 1, 11, I=I)
+    Wl, Ul = _gibbs_literal(b, y, sigma, n, r, q, 3, 1, 11, I)
+    assert (I2 == I).all()
+    assert np.abs(W - Wl).max() <= 1e-10 * np.abs(Wl).max()
+    assert np.abs(U - Ul).max() <= 1e-10 * np.abs(Ul).max()
+
+
+def test_tgp_draws_and_conditional_mean():
+    """I in 1..r with every value used; U init scale sqrt(1/r); the W draw is centred on the
+    posterior mean with covariance M⁻¹ (checked through whitening by chol(M)ᵀ)."""
+    I = R.tgp_draw_I(400, 3, 5, 3)
+    assert I.min() == 1 and I.max() == 5 and I.shape == (400, 3)
+    assert abs(np.bincount(I.ravel())[1:].mean() - 240) < 1e-9
+    U = R.tgp_init_U(200, 5, 2, 3)
+    assert abs(U.std() - math.sqrt(1 / 5)) < 0.02
+    rng = np.random.default_rng(6)
+    n, D, N, r, q, sigma = 5, 2, 40, 3, 7, 0.3
+    b = rng.standard_normal((n, D, N))
+    y = rng.standard_normal(N)
+    I = R.tgp_draw_I(q, D, r, 4)
+    W, U, _ = R.GPT_inf(b, y, sigma, n, r, q, 1, 0, 4, I=I)
+    V = R.tgp_V(U[..., 0], I, b)
+    M = V @ V.T / sigma ** 2 + np.eye(q) * q / r ** D
+    mu = np.linalg.solve(M, V @ y / sigma ** 2)
+    z = np.linalg.cholesky(M).T @ (W[:, 0] - mu)
+    assert np.abs(z - px.normals(q, 4, 0, px.TGP_W_NOISE, 0)).max() < 1e-9
