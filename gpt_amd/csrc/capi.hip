@@ -195,7 +195,7 @@ struct gpt_sgld_session {
   int graph_steps = 0;
   bool store = false, diag = false;
   int engine = 0;                     // kEngineGrid / kEngineChain
-  DevMem segpos;
+  DevMem runq;
 };
 
 // Engine choice: store_flags bit 2 forces the grid engine (sgld.hip), bit 3 the chain engine
@@ -232,15 +232,16 @@ static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t 
 
 // Chain engine tables: for every dimension k the core entries ordered by (I[q,k], q):
 // pos[q + Q*k] = rank of q, seg[k*(r+1) + l] = first rank with I[q,k] = l (0-based).
-static void chain_segpos(const std::vector<int32_t>& I0, int Q, int D, int r,
-                         std::vector<int32_t>& out) {
-  out.assign((size_t)Q * D + (size_t)D * (r + 1), 0);
+// Run members of the chain engine's core sums (see gpt_internal.h StepParams::runq).
+static void chain_runq(const std::vector<int32_t>& I0, int Q, int D, int r,
+                       std::vector<int32_t>& out) {
+  out.assign((size_t)D * r * 64, 256);
   for (int k = 0; k < D; ++k) {
-    std::vector<int> cnt(r + 1, 0);
-    for (int q = 0; q < Q; ++q) cnt[I0[q + (size_t)Q * k] + 1]++;
-    for (int l = 0; l < r; ++l) cnt[l + 1] += cnt[l];
-    for (int l = 0; l <= r; ++l) out[(size_t)Q * D + (size_t)k * (r + 1) + l] = cnt[l];
-    for (int q = 0; q < Q; ++q) out[q + (size_t)Q * k] = cnt[I0[q + (size_t)Q * k]]++;
+    std::vector<int> cnt(r, 0);
+    for (int q = 0; q < Q; ++q) {
+      const int l = I0[q + (size_t)Q * k];
+      out[((size_t)k * r + l) * 64 + cnt[l]++] = q;   // max run <= 64 (chain_supported)
+    }
   }
 }
 
@@ -336,13 +337,13 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   HIPCHK(s->I0.alloc(sizeof(int32_t) * I0.size()));
   HIPCHK(hipMemcpy(s->I0.p, I0.data(), sizeof(int32_t) * I0.size(), hipMemcpyHostToDevice));
   P.I0 = s->I0.as<int32_t>();
-  P.segpos = nullptr;
+  P.runq = nullptr;
   if (s->engine == kEngineChain) {
-    std::vector<int32_t> sp;
-    chain_segpos(I0, Q, D, r, sp);
-    HIPCHK(s->segpos.alloc(sizeof(int32_t) * sp.size()));
-    HIPCHK(hipMemcpy(s->segpos.p, sp.data(), sizeof(int32_t) * sp.size(), hipMemcpyHostToDevice));
-    P.segpos = s->segpos.as<int32_t>();
+    std::vector<int32_t> rq;
+    chain_runq(I0, Q, D, r, rq);
+    HIPCHK(s->runq.alloc(sizeof(int32_t) * rq.size()));
+    HIPCHK(hipMemcpy(s->runq.p, rq.data(), sizeof(int32_t) * rq.size(), hipMemcpyHostToDevice));
+    P.runq = s->runq.as<int32_t>();
   }
   P.stamps = nullptr;
   P.rms = 0; P.rms_eps = 0.0; P.rms_alpha = 0.0;

@@ -12,10 +12,10 @@
 // and, per wave with no block barrier, the Langevin drive, Stiefel projection, geodesic (two Padé
 // expm on the wave) and renormalisation of U^(k) in registers.
 //
-// The A sums are segmented: for every k the core entries q are ordered by (I[q,k], q) on the host
-// (segpos), so A[l,k,row] is a contiguous run of w_q·V_q/temp[k,I[q,k],row] — fixed order, no
-// atomics.  1/temp is formed once per (k, l, row) when temp is, so the Q·D divisions of
-// computeU_phi become multiplications.
+// The core sums A[l,k,row] = Σ_{q: I[q,k]=l} w_q·V_q/temp[k,l,row] are formed as
+// (Σ_{q in run (k,l)} w_q·V_q) · (1/temp[k,l,row]): the V tasks write w_q·V_q once per (row, q)
+// and the run members (host table runq, q ascending) are gathered by 8-lane groups — fixed
+// order, no atomics, and 1/temp is formed once per (k, l, row) when temp is.
 #include "device_util.h"
 
 namespace gpt {
@@ -26,26 +26,31 @@ namespace gpt {
 #ifndef CHAIN_EXP_NOV
 #define CHAIN_EXP_NOV 0
 #endif
-#ifndef CHAIN_ITREG              // V-task table entries held in registers across the batch
-#define CHAIN_ITREG 1
+#ifndef CHAIN_PRIO                // s_setprio 1 for the second-dispatched half of the waves
+#define CHAIN_PRIO 0
 #endif
 #ifndef CHAIN_STAGE_AT
 #define CHAIN_STAGE_AT 3          // next group's rows staged at: 0 (a), 1 (c), 2 (e), 3 end of (b), 4 end of (c)
 #endif
+#ifndef CHAIN_DBUF                // two row-staging buffers: group g+1 is staged at the top of
+#define CHAIN_DBUF 0              // iteration g and (e) re-reads its rows from LDS
+#endif
+constexpr int kChainBufs = CHAIN_DBUF ? 2 : 1;
 constexpr int kChainDMax = 8;     // waves per workgroup (one per input dimension)
 constexpr int kChainTasks = 2;    // V-phase tasks per wave (NCH·G <= tasks·D); J = 8: 1
 constexpr int kChainG = 2;        // batch rows per group
 constexpr int kChainQPL = 4;      // q chunks of 64 (Q <= 64·kChainQPL)
 constexpr int kChainQP = 64 * kChainQPL;
-constexpr int kChainRun = 64;     // slots per run (core entries with one value of I[·,k]) per row
-constexpr int kChainRunS = 72;    // run stride (doubles): 8-lane readers of runs l, l+1.. hit
-                                  // disjoint LDS bank ranges (72·2 dwords ≡ 16 banks mod 64)
+constexpr int kChainRun = 64;     // members per run (core entries with one value of I[·,k])
+constexpr int kChainRunS = 72;    // reduction scratch stride (doubles): 8-lane readers of rows
+                                  // l, l+1.. hit disjoint LDS bank ranges (72·2 dwords ≡ 16 banks)
+constexpr int kChainQS = 264;     // w·V row stride; slot kChainQP of a row is a constant 0
 
 struct ChainLayout {
   int NCH, NT;                    // q chunks of 64, tasks = NCH·G
   int TS;                         // doubles per temp slot: temp | ones(G) | 1/temp | ones(G)
-  size_t o_IT, o_pos, o_w, o_idx, o_y, o_temp, o_fp, o_gwp, o_misc, o_un, bytes;
-  size_t L_dbl, x_dbl;            // union tenants (doubles): run buffer | per-wave scratch
+  size_t o_IT, o_w, o_idx, o_y, o_temp, o_fp, o_gwp, o_misc, o_un, bytes;
+  size_t L_dbl, x_dbl;            // union tenants (doubles): w·V rows + reduction scratch | per-wave scratch
 };
 
 // Per-wave scratch after the batch: S0 = max(expm<2r> scratch, noise slots) | E[:,1:r] | grams.
@@ -63,7 +68,6 @@ GPT_HD ChainLayout chain_layout(int n, int D, int r, int Q, int m, int G) {
   size_t o = 0;
   // index tables for all kChainDMax dimensions (rows k >= D point at the ones / trash slots)
   L.o_IT = o;   o = al16(o + 4 * (size_t)Q * kChainDMax);
-  L.o_pos = o;  o = al16(o + 4 * (size_t)Q * kChainDMax);
   L.o_w = o;    o = al16(o + 8 * (size_t)Q);
   L.o_idx = o;  o = al16(o + 4 * (size_t)m);
   L.o_y = o;    o = al16(o + 8 * (size_t)m);
@@ -72,8 +76,8 @@ GPT_HD ChainLayout chain_layout(int n, int D, int r, int Q, int m, int G) {
   L.o_gwp = o;  o = al16(o + 8 * (size_t)L.NT * 64);
   L.o_misc = o; o = al16(o + 8 * 16);
   L.o_un = o;
-  // batch-loop tenants: runs [k][row][l][slot] (stride kChainRunS) | per-wave reduction scratch
-  L.L_dbl = (size_t)kChainDMax * G * r * kChainRunS + (size_t)D * r * kChainRunS;
+  // batch-loop tenants: w·V rows [row][q] (stride kChainQS) | per-wave reduction scratch
+  L.L_dbl = (size_t)G * kChainQS + (size_t)D * r * kChainRunS;
   L.x_dbl = chain_scratch_dbl(r);
   const size_t un = 8 * (L.L_dbl > L.x_dbl * D ? L.L_dbl : L.x_dbl * D);
   L.bytes = al16(o + un);
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
                                                                 const long long* __restrict__ tbase,
                                                                 int t_local) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ __attribute__((aligned(16))) double pbuf[kChainDMax * G * 64 * J];   // row staging
+  __shared__ __attribute__((aligned(16))) double pbuf[kChainBufs * kChainDMax * G * 64 * J];   // row staging
   // Chain fields are read through Cp at their point of use (scalar loads) rather than held in
   // SGPRs across the batch loop, where SGPR pressure spills into VGPR lanes.
   const ChainDesc* Cp = chains + blockIdx.x;
@@ -137,7 +141,6 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   const int n = P.n, D = P.D, Q = P.Q, m = P.m, NTH = 64 * D;
   const ChainLayout L = chain_layout(n, D, R, Q, m, G);
   int* IT_l = (int*)(smem + L.o_IT);
-  int* pos_l = (int*)(smem + L.o_pos);
   double* w_l = (double*)(smem + L.o_w);
   int* idx_l = (int*)(smem + L.o_idx);
   double* y_l = (double*)(smem + L.o_y);
@@ -146,37 +149,28 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   double* gwp_l = (double*)(smem + L.o_gwp);
   double* misc = (double*)(smem + L.o_misc);
   int* flag = (int*)(misc + 8);
-  double* Lseg = (double*)(smem + L.o_un);
+  double* wVr = (double*)(smem + L.o_un);                       // w_q·V_q per batch row
   double* X = (double*)(smem + L.o_un) + (size_t)k * L.x_dbl;   // this wave's scratch
   double* xi_l = X;                                             // noise slots (before expm)
-  double* pw = pbuf + k * (G * 64 * J);                         // this wave's staged rows
-  double* bscr = Lseg + (size_t)kChainDMax * G * R * kChainRunS + (size_t)k * R * kChainRunS;
+  double* pw0 = pbuf + k * (kChainBufs * G * 64 * J);           // this wave's staged rows
+  double* bscr = wVr + (size_t)G * kChainQS + (size_t)k * R * kChainRunS;
 
   const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
   if (__hip_atomic_load(Cp->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   CSTAMP(0);
+  if (CHAIN_PRIO && k >= 4) __builtin_amdgcn_s_setprio(1);
 
   // ---- prologue: index tables, w, batch rows, and U^(k) into registers
   const int DRG = D * R * G;
   {
     // IT_l[kk·Q+q]: temp index (kk·R + I[q,kk])·G of the core entry (+gg at use); rows kk >= D
-    // point at the ones slot.  pos_l: run slot ((kk·G)·R + l)·64 + (rank of q within run l)
-    // (+gg·R·64 at use), l = I[q,kk]; rows kk >= D land in never-read trash rows.
-    const int32_t* segp = P.segpos + (size_t)Q * D;
+    // point at the ones slot.
     for (int o = tid; o < Q * kChainDMax; o += NTH) {
       const int kk = o / Q, q = o - kk * Q;
-      if (kk < D) {
-        const int l = gptr(P.I0)[q + Q * kk];
-        IT_l[o] = (kk * R + l) * G;
-        pos_l[o] = (kk * G * R + l) * kChainRunS +
-                   (gptr(P.segpos)[q + Q * kk] - gptr(segp)[kk * (R + 1) + l]);
-      } else {
-        IT_l[o] = DRG;
-        pos_l[o] = kk * G * R * kChainRunS;
-      }
+      IT_l[o] = kk < D ? (kk * R + gptr(P.I0)[q + Q * kk]) * G : DRG;
     }
-    for (int o = tid; o < D * G * R * kChainRunS; o += NTH) Lseg[o] = 0.0;  // empty slots read 0
+    for (int o = tid; o < G; o += NTH) wVr[o * kChainQS + kChainQP] = 0.0;   // gather zero slots
     for (int o = tid; o < 2 * G; o += NTH) {                     // ones slots of both temp slots
       temp_l[o / G * L.TS + DRG + o % G] = 1.0;
       temp_l[o / G * L.TS + 2 * DRG + G + o % G] = 1.0;
@@ -218,7 +212,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   const double* phi_k = uni_ptr(Cp->phi) + koff;
   // Stage rows g0n .. g0n+G-1 of this wave's dimension into pw (lane-linear LDS image: double j
   // of row gg at pw[gg·64J + j]); bytes past the row end are clamped in-row and never read.
-  auto stage = [&](int g0n, int ln) {
+  auto stage = [&](int g0n, int ln, double* pw) {
     int rows[G];
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) rows[gg] = uni(idx_l[min(g0n + gg, Bt - 1)]);
@@ -248,7 +242,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       }
     }
   };
-  stage(0, lane);
+  stage(0, lane, pw0);
 
 
   double acc[J][R];
@@ -261,19 +255,31 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #pragma unroll
   for (int x = 0; x < TPW; ++x) { vsave[x] = 0.0; gw[x] = 0.0; }
 
-#if CHAIN_ITREG
-  // this wave's V-task table entries, packed (temp index | run slot << 12), fixed for the step
-  int itps[TPW][kChainDMax];
+  // this wave's V-task temp indices (< 256, four per register), fixed for the step
+  unsigned itp[TPW][kChainDMax / 4];
 #pragma unroll
   for (int x = 0; x < TPW; ++x) {
     const int task = k + D * x;
     const int c = task < L.NT ? task % L.NCH : 0;
     const int qq = min(64 * c + lane, Q - 1);
 #pragma unroll
-    for (int kk = 0; kk < kChainDMax; ++kk)
-      itps[x][kk] = IT_l[kk * Q + qq] | (pos_l[kk * Q + qq] << 12);
+    for (int h = 0; h < kChainDMax / 4; ++h) {
+      unsigned v = 0;
+#pragma unroll
+      for (int b4 = 0; b4 < 4; ++b4) v |= (unsigned)IT_l[(4 * h + b4) * Q + qq] << (8 * b4);
+      itp[x][h] = v;
+    }
   }
-#endif
+  // this lane's run members for the core sums of dimension k: lane 8l+s gathers members
+  // s, s+8, .., s+56 of run (k, l) (two 16-bit q indices per register)
+  unsigned gq[4];
+  {
+    const int rl0 = min(lane >> 3, R - 1), rs0 = lane & 7;
+    const int32_t* rq = P.runq + ((size_t)k * R + rl0) * kChainRun + rs0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      gq[i] = (unsigned)gptr(rq)[16 * i] | ((unsigned)gptr(rq)[16 * i + 8] << 16);
+  }
   int slot = 0;
   for (int g0 = 0; g0 < Bt; g0 += G, slot ^= 1) {
     // lane id the compiler cannot see through: per-lane addresses are recomputed inside the
@@ -282,6 +288,10 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
     asm volatile("" : "+v"(ln));
     // (a) this wave's staged rows -> registers, then stage the next group behind them
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    double* pw = pw0 + (CHAIN_DBUF ? slot * (G * 64 * J) : 0);
+#if CHAIN_DBUF
+    if (g0 + G < Bt) stage(g0 + G, ln, pw0 + (slot ^ 1) * (G * 64 * J));
+#endif
     double p[G][J];
 #pragma unroll
     for (int gg = 0; gg < G; ++gg)
@@ -289,8 +299,8 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       for (int jj = 0; jj < J; ++jj)
         p[gg][jj] = pw[gg * 64 * J + ln + 64 * jj];   // j >= n: finite in-row values, u = 0 there
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#if CHAIN_STAGE_AT == 0
-    if (g0 + G < Bt) stage(g0 + G, ln);
+#if CHAIN_STAGE_AT == 0 && !CHAIN_DBUF
+    if (g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
     // (b) temp[k,l,row] and 1/temp for the G rows: R partial dots per lane, reduced through this
     // wave's LDS scratch by 8-lane groups (lane 8l+s sums 8 partials of output l, DPP finishes)
@@ -317,12 +327,12 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
         tsl[DRG + G + (k * R + rl) * G + gg] = 1.0 / sacc;
       }
     }
-#if CHAIN_STAGE_AT == 3
-    if (g0 + G < Bt) stage(g0 + G, ln);
+#if CHAIN_STAGE_AT == 3 && !CHAIN_DBUF
+    if (g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
     lds_barrier();
-#if CHAIN_STAGE_AT == 1
-    if (g0 + G < Bt) stage(g0 + G, ln);
+#if CHAIN_STAGE_AT == 1 && !CHAIN_DBUF
+    if (g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
     // (c) V tasks: task = gg·NCH + c covers q = 64c + lane of batch column g0+gg
 #pragma unroll
@@ -334,40 +344,23 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       const bool ok = q < Q;
       const int qq = ok ? q : 0;
       // every LDS read of the task in flight at once: kChainDMax dimensions, no guards (rows
-      // kk >= D of the tables hit the ones slots / trash rows)
-      int it[kChainDMax], ps[kChainDMax];
-#if CHAIN_ITREG
-#pragma unroll
-      for (int kk = 0; kk < kChainDMax; ++kk) {
-        it[kk] = (itps[x][kk] & 0xfff) + gg;
-        ps[kk] = (itps[x][kk] >> 12) + gg * R * kChainRunS;
-      }
-#else
-#pragma unroll
-      for (int kk = 0; kk < kChainDMax; ++kk) {
-        it[kk] = IT_l[kk * Q + qq] + gg;
-        ps[kk] = pos_l[kk * Q + qq] + gg * R * kChainRunS;
-      }
-#endif
+      // kk >= D of the table hit the ones slots)
       double V = 1.0;                              // Π_k temp in k order (computeV)
 #pragma unroll
-      for (int kk = 0; kk < kChainDMax; ++kk) V *= tsl[it[kk]];
+      for (int kk = 0; kk < kChainDMax; ++kk)
+        V *= tsl[((itp[x][kk >> 2] >> (8 * (kk & 3))) & 0xff) + gg];
       const double wV = ok ? w_l[qq] * V : 0.0;
-      if (ok) {
-#pragma unroll
-        for (int kk = 0; kk < kChainDMax; ++kk)    // w_q · V / temp[k] (computeU_phi :253)
-          Lseg[ps[kk]] = wV * tsl[it[kk] + DRG + G];
-      }
+      if (ok) wVr[gg * kChainQS + q] = wV;         // w_q·V_q, gathered by the run sums in (e)
       vsave[x] = ok ? V : 0.0;
       const double fs = wave_sum(wV);
       if (lane == 0) fp_l[gg * kChainQPL + c] = fs;
     }
-#if CHAIN_STAGE_AT == 4
-    if (g0 + G < Bt) stage(g0 + G, ln);
+#if CHAIN_STAGE_AT == 4 && !CHAIN_DBUF
+    if (g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
     lds_barrier();
-#if CHAIN_STAGE_AT == 2
-    if (!CHAIN_EXP_NOSTAGE && g0 + G < Bt) stage(g0 + G, ln);
+#if CHAIN_STAGE_AT == 2 && !CHAIN_DBUF
+    if (!CHAIN_EXP_NOSTAGE && g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
     // (e) residuals, A[:,k,·]·res, and the gradU / gradw accumulation
     double res[G];
@@ -380,18 +373,26 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
     }
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
-      // A[l,k,row] = Σ of run l of this row's run slots: lane 8l+s sums slots s, s+8, ..., the
-      // 8-lane group finishes with DPP; lane 8l then holds A[l]
-      const double* Lp = Lseg + ((k * G + gg) * R + rl) * kChainRunS + rs;
+      // A[l,k,row] = (Σ_{q in run (k,l)} w_q·V_q) / temp[k,l,row] (computeU_phi + computeA,
+      // :248-273): lane 8l+s sums members s, s+8, .., the 8-lane group finishes with DPP; lane
+      // 8l then holds A[l]
+      const double* wr = wVr + gg * kChainQS;
       double a = 0.0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a += Lp[8 * i];
-      a = group8_sum(a);
+      for (int i = 0; i < 8; ++i) a += wr[(gq[i >> 1] >> (16 * (i & 1))) & 0xffff];
+      a = group8_sum(a) * tsl[DRG + G + (k * R + rl) * G + gg];
+      double cc[R];
 #pragma unroll
-      for (int l = 0; l < R; ++l) {
-        const double cc = readlane_d(a, 8 * l) * res[gg];
+      for (int l = 0; l < R; ++l) cc[l] = readlane_d(a, 8 * l) * res[gg];
 #pragma unroll
-        for (int jj = 0; jj < J; ++jj) acc[jj][l] = fma(p[gg][jj], cc, acc[jj][l]);
+      for (int jj = 0; jj < J; ++jj) {
+#if CHAIN_DBUF
+        const double pv = pw[gg * 64 * J + ln + 64 * jj];
+#else
+        const double pv = p[gg][jj];
+#endif
+#pragma unroll
+        for (int l = 0; l < R; ++l) acc[jj][l] = fma(pv, cc[l], acc[jj][l]);
       }
     }
 #pragma unroll
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   X(4, 1) X(4, 2) X(4, 4) X(4, 8) X(5, 1) X(5, 2) X(5, 4) X(5, 8)
 
 // Static LDS of chain_kernel<R, J, G>: the row staging buffer.
-static size_t chain_static_lds(int J) { return 8 * (size_t)kChainDMax * kChainG * 64 * J; }
+static size_t chain_static_lds(int J) { return 8 * (size_t)kChainBufs * kChainDMax * kChainG * 64 * J; }
 
 static int chain_J(int n) { return n <= 64 ? 1 : (n <= 128 ? 2 : (n <= 256 ? 4 : (n <= 512 ? 8 : 0))); }
 

@@ -47,8 +47,8 @@ struct StepParams {
   int store_every;
   int langevin, stiefel;
   const int32_t* I0;              // Q*D 0-based, layout q + Q*k
-  const int32_t* segpos;          // chain engine: pos (Q*D, rank of q in the (I[q,k], q) order of
-                                  // dimension k, layout q + Q*k) then seg (D*(r+1) run starts)
+  const int32_t* runq;            // chain engine: runq[(k*r + l)*64 + s] = s-th q (ascending) with
+                                  // I[q,k] = l, or 256 (a zero slot) past the run's end
   long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
   int rms;                        // 1: GPT_SGLDERM_RMSprop steps (grid engine, two launches)
   double rms_eps, rms_alpha;      // its epsilon and moving-average coefficient

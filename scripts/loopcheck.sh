@@ -2,7 +2,7 @@
 # Spill / wait report of the chain kernel's batch loop (R, J given), e.g. scripts/loopcheck.sh 5 8
 R=${1:-5}; J=${2:-8}
 d=$(mktemp -d); cd $d
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics --save-temps=obj -c /root/repo/gpt_amd/csrc/chain.hip -o x.o 2>/dev/null
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics $EXTRA --save-temps=obj -c /root/repo/gpt_amd/csrc/chain.hip -o x.o 2>/dev/null
 F=$(ls *gfx950.s)
 L0=$(grep -n "^_ZN3gpt12chain_kernelILi${R}ELi${J}ELi2E.*:" $F | head -1 | cut -d: -f1)
 L1=$(awk -v s=$L0 'NR>s && /s_endpgm/ {print NR; exit}' $F)
