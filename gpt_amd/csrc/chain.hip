@@ -77,7 +77,7 @@ GPT_HD ChainLayout chain_layout(int n, int D, int r, int Q, int m, int G) {
   L.o_misc = o; o = al16(o + 8 * 16);
   L.o_un = o;
   // batch-loop tenants: w·V rows [row][q] (stride kChainQS) | per-wave reduction scratch
-  L.L_dbl = (size_t)G * kChainQS + (size_t)D * r * kChainRunS;
+  L.L_dbl = (size_t)G * kChainQS + (size_t)D * G * r * kChainRunS;
   L.x_dbl = chain_scratch_dbl(r);
   const size_t un = 8 * (L.L_dbl > L.x_dbl * D ? L.L_dbl : L.x_dbl * D);
   L.bytes = al16(o + un);
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   double* X = (double*)(smem + L.o_un) + (size_t)k * L.x_dbl;   // this wave's scratch
   double* xi_l = X;                                             // noise slots (before expm)
   double* pw0 = pbuf + k * (kChainBufs * G * 64 * J);           // this wave's staged rows
-  double* bscr = wVr + (size_t)G * kChainQS + (size_t)k * R * kChainRunS;
+  double* bscr = wVr + (size_t)G * kChainQS + (size_t)k * G * R * kChainRunS;   // per row
 
   const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
@@ -161,63 +161,15 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   CSTAMP(0);
   if (CHAIN_PRIO && k >= 4) __builtin_amdgcn_s_setprio(1);
 
-  // ---- prologue: index tables, w, batch rows, and U^(k) into registers
-  const int DRG = D * R * G;
-  {
-    // IT_l[kk·Q+q]: temp index (kk·R + I[q,kk])·G of the core entry (+gg at use); rows kk >= D
-    // point at the ones slot.
-    for (int o = tid; o < Q * kChainDMax; o += NTH) {
-      const int kk = o / Q, q = o - kk * Q;
-      IT_l[o] = kk < D ? (kk * R + gptr(P.I0)[q + Q * kk]) * G : DRG;
-    }
-    for (int o = tid; o < G; o += NTH) wVr[o * kChainQS + kChainQP] = 0.0;   // gather zero slots
-    for (int o = tid; o < 2 * G; o += NTH) {                     // ones slots of both temp slots
-      temp_l[o / G * L.TS + DRG + o % G] = 1.0;
-      temp_l[o / G * L.TS + 2 * DRG + G + o % G] = 1.0;
-    }
-    for (int o = tid; o < kChainQPL * G; o += NTH) fp_l[o] = 0.0;
-  }
-  for (int q = tid; q < Q; q += NTH) w_l[q] = gptr(Cp->w)[(size_t)(t & 1) * Q + q];
-  if (tid == 0) flag[0] = 0;
   const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
   const int start = b * m;
   const int Bt = min(m, P.N - start);
-  {
-    const int32_t* ord = Cp->order + (size_t)e * P.N + start;
-    const double* yv = Cp->y;
-    for (int i = tid; i < Bt; i += NTH) {
-      const int row = gptr(ord)[i];
-      idx_l[i] = row;
-      y_l[i] = gptr(yv)[row];
-    }
-  }
-  double u[J][R];
-  {
-    const double* Ug = Cp->U + (size_t)n * R * k;
-#pragma unroll
-    for (int jj = 0; jj < J; ++jj) {
-      const int j = lane + 64 * jj;
-      const int jc = min(j, n - 1);          // unconditional in-bounds loads, padding rows zeroed
-#pragma unroll
-      for (int l = 0; l < R; ++l) {
-        const double x = gptr(Ug + (size_t)n * l)[jc];
-        u[jj][l] = j < n ? x : 0.0;
-      }
-    }
-  }
-  __syncthreads();
-  CSTAMP(1);
-
+  const int32_t* ord = Cp->order + (size_t)e * P.N + start;
   const long long koff = (long long)n * k, rstride = (long long)n * D;
   const double* phi_k = uni_ptr(Cp->phi) + koff;
   // Stage rows g0n .. g0n+G-1 of this wave's dimension into pw (lane-linear LDS image: double j
   // of row gg at pw[gg·64J + j]); bytes past the row end are clamped in-row and never read.
-  auto stage = [&](int g0n, int ln, double* pw) {
-    int rows[G];
-#pragma unroll
-    for (int gg = 0; gg < G; ++gg) rows[gg] = uni(idx_l[min(g0n + gg, Bt - 1)]);
-    // no LDS read between the DMA issues below: a DS read after a pending LDS-DMA may be
-    // ordered behind it (vmcnt) by the compiler
+  auto stage_rows = [&](const int (&rows)[G], int ln, double* pw) {
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
       const char* rb = (const char*)(phi_k + (long long)rows[gg] * rstride);
@@ -242,7 +194,65 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       }
     }
   };
-  stage(0, lane, pw0);
+  auto stage = [&](int g0n, int ln, double* pw) {
+    int rows[G];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) rows[gg] = uni(idx_l[min(g0n + gg, Bt - 1)]);
+    // no LDS read between the DMA issues: a DS read after a pending LDS-DMA may be ordered
+    // behind it (vmcnt) by the compiler
+    stage_rows(rows, ln, pw);
+  };
+  {
+    // the first group's rows go out before the prologue's own loads (row indices from global)
+    int rows0[G];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) rows0[gg] = gptr(ord)[min(gg, Bt - 1)];
+    stage_rows(rows0, lane, pw0);
+  }
+
+  // ---- prologue: index tables, w, batch rows, and U^(k) into registers
+  const int DRG = D * R * G;
+  {
+    // IT_l[kk·Q+q]: temp index (kk·R + I[q,kk])·G of the core entry (+gg at use); rows kk >= D
+    // point at the ones slot.
+    for (int o = tid; o < Q * kChainDMax; o += NTH) {
+      const int kk = o / Q, q = o - kk * Q;
+      IT_l[o] = kk < D ? (kk * R + gptr(P.I0)[q + Q * kk]) * G : DRG;
+    }
+    for (int o = tid; o < G; o += NTH) wVr[o * kChainQS + kChainQP] = 0.0;   // gather zero slots
+    for (int o = tid; o < 2 * G; o += NTH) {                     // ones slots of both temp slots
+      temp_l[o / G * L.TS + DRG + o % G] = 1.0;
+      temp_l[o / G * L.TS + 2 * DRG + G + o % G] = 1.0;
+    }
+    for (int o = tid; o < kChainQPL * G; o += NTH) fp_l[o] = 0.0;
+  }
+  for (int q = tid; q < Q; q += NTH) w_l[q] = gptr(Cp->w)[(size_t)(t & 1) * Q + q];
+  if (tid == 0) flag[0] = 0;
+  {
+    const double* yv = Cp->y;
+    for (int i = tid; i < Bt; i += NTH) {
+      const int row = gptr(ord)[i];
+      idx_l[i] = row;
+      y_l[i] = gptr(yv)[row];
+    }
+  }
+  double u[J][R];
+  {
+    const double* Ug = Cp->U + (size_t)n * R * k;
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = lane + 64 * jj;
+      const int jc = min(j, n - 1);          // unconditional in-bounds loads, padding rows zeroed
+#pragma unroll
+      for (int l = 0; l < R; ++l) {
+        const double x = gptr(Ug + (size_t)n * l)[jc];
+        u[jj][l] = j < n ? x : 0.0;
+      }
+    }
+  }
+  __syncthreads();
+  CSTAMP(1);
+
 
 
   double acc[J][R];
@@ -316,15 +326,22 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #pragma unroll
         for (int l = 0; l < R; ++l) v[l] = fma(p[gg][jj], u[jj][l], v[l]);
 #pragma unroll
-      for (int l = 0; l < R; ++l) bscr[l * kChainRunS + ln] = v[l];
-      wave_sync();
-      double sacc = 0.0;
+      for (int l = 0; l < R; ++l) bscr[(gg * R + l) * kChainRunS + ln] = v[l];
+    }
+    wave_sync();
+    double sacc[G];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) sacc += bscr[rl * kChainRunS + rs + 8 * i];
-      sacc = group8_sum(sacc);
+    for (int gg = 0; gg < G; ++gg) {
+      sacc[gg] = 0.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sacc[gg] += bscr[(gg * R + rl) * kChainRunS + rs + 8 * i];
+    }
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      const double sv = group8_sum(sacc[gg]);
       if (rs == 0 && (ln >> 3) < R) {
-        tsl[(k * R + rl) * G + gg] = sacc;
-        tsl[DRG + G + (k * R + rl) * G + gg] = 1.0 / sacc;
+        tsl[(k * R + rl) * G + gg] = sv;
+        tsl[DRG + G + (k * R + rl) * G + gg] = 1.0 / sv;
       }
     }
 #if CHAIN_STAGE_AT == 3 && !CHAIN_DBUF
@@ -345,10 +362,12 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       const int qq = ok ? q : 0;
       // every LDS read of the task in flight at once: kChainDMax dimensions, no guards (rows
       // kk >= D of the table hit the ones slots)
-      double V = 1.0;                              // Π_k temp in k order (computeV)
+      double tv[kChainDMax];                       // Π_k temp (computeV), as a product tree
 #pragma unroll
       for (int kk = 0; kk < kChainDMax; ++kk)
-        V *= tsl[((itp[x][kk >> 2] >> (8 * (kk & 3))) & 0xff) + gg];
+        tv[kk] = tsl[((itp[x][kk >> 2] >> (8 * (kk & 3))) & 0xff) + gg];
+      static_assert(kChainDMax == 8, "product tree below is written for 8 dimensions");
+      const double V = ((tv[0] * tv[1]) * (tv[2] * tv[3])) * ((tv[4] * tv[5]) * (tv[6] * tv[7]));
       const double wV = ok ? w_l[qq] * V : 0.0;
       if (ok) wVr[gg * kChainQS + q] = wV;         // w_q·V_q, gathered by the run sums in (e)
       vsave[x] = ok ? V : 0.0;

@@ -479,10 +479,11 @@ __device__ bool wave_expm(double* S) {
     }
     wave_sync();
     for (int kk = 1; kk <= (deg - 1) / 2; ++kk) {
-      wave_mm<NN>(T, A2, A4);  // P = P·A2  (A4 is free scratch here)
+      if (kk > 1) wave_mm<NN>(T, A2, A4);   // P = P·A2 (A4 is free scratch here); P1 = A2
+      const double* Pk = kk > 1 ? A4 : A2;
       const double cu = C[2 * kk + 1], cv = C[2 * kk];
       for (int o = lane; o < q; o += 64) {
-        const double p = A4[o];
+        const double p = Pk[o];
         T[o] = p;
         U[o] = U[o] + cu * p;
         V[o] = V[o] + cv * p;
