@@ -12,6 +12,7 @@ Same function names, argument meaning, return values and error behaviour as the 
     GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch[, param_seed];
                   langevin, stiefel)                          GPT_SGLD.jl:345
     GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch)  GPT_SGLD_p.jl:146
+    GPT_SGLDERMw(phi, y, signal_var, I, r, Q, m, epsw, burnin, maxepoch)  GPT_SGLD.jl:1065
     pred(w, U, I, phitest)                                    GPT_SGLD.jl:233
     RMSE(w_store, U_store, I, phitest, ytest)                 GPT_SGLD_p.jl:124
     GPNT_SGLD(phi, y, signal_var, sigma_theta, m, eps_theta, decay_rate, burnin, maxepoch,
@@ -242,6 +243,33 @@ def GPT_SGLDERM_RMSprop(phi, y, signal_var, I, r, Q, m, epsilon, alpha, burnin, 
     else:
         check(code)
     return (w_store, U_store, dg) if diag else (w_store, U_store)
+
+
+def GPT_SGLDERMw(phi, y, signal_var, I, r, Q, m, epsw, burnin, maxepoch, param_seed=0,
+                 w_init=None, U_init=None, diag=False):
+    """SGLD on w with U fixed at its uniform Stiefel draw (GPT_SGLD.jl:1065-1118).  Returns
+    (w_store, U) [, gradw norms per step]."""
+    phi = _f64(phi)
+    n, D, N = phi.shape
+    y = _f64(np.asarray(y, dtype=np.float64).ravel())
+    if y.size != N:
+        raise ValueError("phi and y disagree on N")
+    I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+    if I.shape != (Q, D):
+        raise ValueError("I must be (Q, D)")
+    cfg = make_config(n, D, N, r, Q, m, epsw, 0.0, signal_var, 1.0, burnin, maxepoch,
+                      param_seed, True, True, 1, 0)
+    nb = -(-N // m)
+    w_store = np.zeros((Q, maxepoch * nb), order="F")
+    U = np.zeros((n, r, D), order="F")
+    dg = np.zeros((1 + D, (burnin + maxepoch) * nb), order="F") if diag else None
+    wi = _f64(w_init) if w_init is not None else None
+    Ui = _f64(U_init) if U_init is not None else None
+    check(lib().gpt_sgld_wonly(C.byref(cfg), _ptr(phi), _ptr(y), _ptr(I, P_I32),
+                               _ptr(wi) if wi is not None else None,
+                               _ptr(Ui) if Ui is not None else None, _ptr(w_store), _ptr(U),
+                               _ptr(dg) if diag else None))
+    return (w_store, U, dg[0].copy()) if diag else (w_store, U)
 
 
 def GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0, **kw):

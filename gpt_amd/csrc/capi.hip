@@ -198,7 +198,7 @@ struct gpt_sgld_session {
   DevMem runq;
 };
 
-// Engine choice: store_flags bit 2 forces the grid engine (sgld.hip), bit 3 the chain engine
+// Engine choice: store_flags bit 2 (or bit 4, w-only steps) forces the grid engine (sgld.hip), bit 3 the chain engine
 // (chain.hip); otherwise GPTSGLD_ENGINE=grid|chain, otherwise chain whenever it supports the shape.
 static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t flags,
                        int* engine) {
@@ -212,7 +212,7 @@ static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t 
   const bool grid_ok =
       step_layout((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m).bytes <= 160 * 1024;
   int want = -1;
-  if (flags & 4) want = kEngineGrid;
+  if (flags & (4 | 16)) want = kEngineGrid;
   else if (flags & 8) want = kEngineChain;
   else if (const char* ev = std::getenv("GPTSGLD_ENGINE")) {
     if (!std::strcmp(ev, "grid")) want = kEngineGrid;
@@ -258,6 +258,9 @@ extern "C" int gpt_device_count(void) {
 }
 
 static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t_local) {
+  if (P.wonly)
+    return launch_step_wonly(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
+                             t_local, s->stream);
   if (P.rms)
     return launch_step_rms(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
                            t_local, s->stream);
@@ -347,6 +350,7 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   }
   P.stamps = nullptr;
   P.rms = 0; P.rms_eps = 0.0; P.rms_alpha = 0.0;
+  P.wonly = (store_flags & 16) ? 1 : 0;
   HIPCHK(s->tbase.alloc(sizeof(long long)));
   HIPCHK(hipMemset(s->tbase.p, 0, sizeof(long long)));
   HIPCHK(s->status.alloc(sizeof(int32_t) * nchains));
@@ -629,7 +633,7 @@ extern "C" int gpt_sgld_init(const gpt_sgld_config* cfg, double* w_out, double* 
 static int host_sampler(const gpt_sgld_config* cfg, const double* phi, const double* y,
                         const int32_t* I, const double* w_init, const double* U_init,
                         double* w_store, double* U_store, double* diag, int extra_flags,
-                        double rms_eps, double rms_alpha) {
+                        double rms_eps, double rms_alpha, double* U_final = nullptr) {
   if (!valid_cfg(cfg)) return GPT_ERR_BAD_DIMS;
   if (!phi || !y || !I) { set_error("null input"); return GPT_ERR_BAD_DIMS; }
   const size_t nphi = (size_t)cfg->n * cfg->D * cfg->N;
@@ -662,6 +666,9 @@ static int host_sampler(const gpt_sgld_config* cfg, const double* phi, const dou
     set_error("Get NaN when moving along Geodesic. Try smaller epsU");
     return GPT_ERR_NAN_GEODESIC;
   }
+  if (U_final)
+    HIPCHK(hipMemcpy(U_final, s->chains_h[0].U, 8 * (size_t)cfg->n * cfg->r * cfg->D,
+                     hipMemcpyDeviceToHost));
   return GPT_OK;
 }
 
@@ -677,6 +684,16 @@ extern "C" int gpt_sgld_rmsprop(const gpt_sgld_config* cfg, double epsilon, doub
                                 double* U_store, double* diag) {
   if (!(epsilon > 0)) { set_error("RMSprop needs epsilon > 0"); return GPT_ERR_BAD_DIMS; }
   return host_sampler(cfg, phi, y, I, w_init, U_init, w_store, U_store, diag, 4, epsilon, alpha);
+}
+
+extern "C" int gpt_sgld_wonly(const gpt_sgld_config* cfg, const double* phi, const double* y,
+                              const int32_t* I, const double* w_init, const double* U_init,
+                              double* w_store, double* U_out, double* diag) {
+  if (!cfg || !cfg->stiefel || !cfg->langevin) {
+    set_error("GPT_SGLDERMw: U is a uniform Stiefel draw and w takes SGLD steps (stiefel = langevin = 1)");
+    return GPT_ERR_BAD_DIMS;
+  }
+  return host_sampler(cfg, phi, y, I, w_init, U_init, w_store, nullptr, diag, 16, 0.0, 0.0, U_out);
 }
 
 extern "C" int gpt_samplenz(int64_t r, int64_t D, int64_t Q, uint64_t seed, int32_t* I_out) {

@@ -51,6 +51,7 @@ struct StepParams {
                                   // I[q,k] = l, or 256 (a zero slot) past the run's end
   long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
   int rms;                        // 1: GPT_SGLDERM_RMSprop steps (grid engine, two launches)
+  int wonly;                      // 1: GPT_SGLDERMw steps (w alone, U fixed; grid engine)
   double rms_eps, rms_alpha;      // its epsilon and moving-average coefficient
 };
 constexpr int kStamps = 16;       // stamp slots per block
@@ -125,6 +126,8 @@ hipError_t launch_temp_init(const StepParams& P, const ChainDesc* chains, int nc
 hipError_t launch_step(const StepParams& P, const ChainDesc* chains, int nchains,
                        const long long* tbase, int t_local, hipStream_t st);
 // RMSprop step = w phase (one workgroup per chain) then U phase (D workgroups per chain)
+hipError_t launch_step_wonly(const StepParams& P, const ChainDesc* chains, int nchains,
+                             const long long* tbase, int t_local, hipStream_t st);
 hipError_t launch_step_rms(const StepParams& P, const ChainDesc* chains, int nchains,
                            const long long* tbase, int t_local, hipStream_t st);
 hipError_t launch_advance(long long* tbase, long long by, hipStream_t st);

@@ -416,11 +416,12 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
 template <int R>
 __global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
                                                         const ChainDesc* __restrict__ chains,
-                                                        const long long* __restrict__ tbase) {
+                                                        const long long* __restrict__ tbase,
+                                                        int t_local) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const ChainDesc C = chains[blockIdx.y];
   const int k = blockIdx.x, tid = threadIdx.x;
-  const long long t = tbase[0];
+  const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
   const int n = P.n, D = P.D, m = P.m;
   const StepLayout L = step_layout(n, D, R, P.Q, m);
@@ -464,7 +465,7 @@ hipError_t launch_temp_init(const StepParams& P, const ChainDesc* chains, int nc
   switch (P.r) {
 #define CASE(RR)                                                                           \
   case RR:                                                                                 \
-    hipLaunchKernelGGL(temp_init_kernel<RR>, grid, dim3(kNT), L.bytes, st, P, chains, tbase); \
+    hipLaunchKernelGGL(temp_init_kernel<RR>, grid, dim3(kNT), L.bytes, st, P, chains, tbase, 0); \
     break;
     GPT_RANKS(CASE)
 #undef CASE
@@ -500,6 +501,26 @@ hipError_t launch_step_rms(const StepParams& P, const ChainDesc* chains, int nch
                        chains, tbase, t_local, P.D);                                          \
     hipLaunchKernelGGL(sgld_step_kernel<RR>, dim3(P.D, nchains), dim3(kNT), L.bytes, st, P,   \
                        chains, tbase, t_local, 0);                                            \
+    break;
+    GPT_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// GPT_SGLDERMw (GPT_SGLD.jl:1065-1118): U never moves, so each step is temp of its batch with the
+// fixed U (temp_init_kernel) followed by the w block alone.
+hipError_t launch_step_wonly(const StepParams& P, const ChainDesc* chains, int nchains,
+                             const long long* tbase, int t_local, hipStream_t st) {
+  const StepLayout L = step_layout(P.n, P.D, P.r, P.Q, P.m);
+  switch (P.r) {
+#define CASE(RR)                                                                              \
+  case RR:                                                                                    \
+    hipLaunchKernelGGL(temp_init_kernel<RR>, dim3(P.D, nchains), dim3(kNT), L.bytes, st, P,   \
+                       chains, tbase, t_local);                                               \
+    hipLaunchKernelGGL(sgld_step_kernel<RR>, dim3(1, nchains), dim3(kNT), L.bytes, st, P,     \
+                       chains, tbase, t_local, P.D);                                          \
     break;
     GPT_RANKS(CASE)
 #undef CASE

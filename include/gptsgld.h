@@ -89,6 +89,13 @@ int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi, const dou
  * GPT_SGLD.jl:1121-1237: per-entry RMSprop step sizes for w, one averaged step per U^(k), w
  * updated before A.  cfg's epsw/epsU/sigma_w are not used (sigma_w = 1 as in the reference);
  * cfg->langevin and cfg->stiefel must be 1.  Runs on the grid engine. */
+/* GPT_SGLDERMw(phi,y,signal_var,I,r,Q,m,epsw,burnin,maxepoch)  GPT_SGLD.jl:1065-1118: SGLD on w
+ * alone, U fixed at its uniform Stiefel draw (cfg: stiefel = langevin = 1, sigma_w = 1; epsU is
+ * unused).  w_store (Q, maxepoch*numbatches), U_out (n, r, D) = the fixed U, diag row 0 = |gradw|
+ * per step.  Runs on the grid engine (store_flags bit 4 in a session). */
+int gpt_sgld_wonly(const gpt_sgld_config* cfg, const double* phi, const double* y, const int32_t* I,
+                   const double* w_init, const double* U_init, double* w_store, double* U_out,
+                   double* diag);
 int gpt_sgld_rmsprop(const gpt_sgld_config* cfg, double epsilon, double alpha, const double* phi,
                      const double* y, const int32_t* I, const double* w_init,
                      const double* U_init, double* w_store, double* U_store, double* diag);

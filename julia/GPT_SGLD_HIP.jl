@@ -9,7 +9,7 @@
 module GPT_SGLD_HIP
 
 export datawhitening, feature, featureNotensor, samplenz, GPTregression, GPT_SGLDERM, pred, RMSE,
-       GPNT_SGLD, GPT_SGLDERM_RMSprop
+       GPNT_SGLD, GPT_SGLDERM_RMSprop, GPT_SGLDERMw
 
 const LIB = get(ENV, "GPTSGLD_LIB", joinpath(@__DIR__, "..", "gpt_amd", "libgptsgld.so"))
 
@@ -129,6 +129,21 @@ function GPT_SGLDERM_RMSprop(phi::Array{Float64,3}, y::Array{Float64}, signal_va
 end
 
 # pred(w,U,I,phitest)  GPT_SGLD.jl:233
+# GPT_SGLD.jl:1065-1118 (w-only SGLD, U fixed at its Stiefel draw)
+function GPT_SGLDERMw(phi::Array{Float64,3}, y::Array{Float64}, signal_var::Real, I::Array{Int32,2},
+                      r::Integer, Q::Integer, m::Integer, epsw::Real, burnin::Integer, maxepoch::Integer,
+                      param_seed::Integer=0)
+    n, D, N = size(phi)
+    cfg = SGLDConfig(n, D, N, r, Q, m, epsw, 0.0, signal_var, 1.0, burnin, maxepoch, param_seed, 1, 1, 1, 0)
+    w_store = Array{Float64}(undef, Q, maxepoch * cld(N, m))
+    U = Array{Float64}(undef, n, r, D)
+    check(ccall((:gpt_sgld_wonly, LIB), Cint,
+                (Ref{SGLDConfig}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64},
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                cfg, phi, vec(y), I, C_NULL, C_NULL, w_store, U, C_NULL))
+    return w_store, U
+end
+
 function pred(w::Array{Float64}, U::Array{Float64,3}, I::Array{Int32,2}, phitest::Array{Float64,3})
     n, D, Nt = size(phitest); r = size(U, 2); Q = length(w)
     f = Array{Float64}(undef, Nt)

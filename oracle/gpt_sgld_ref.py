@@ -378,6 +378,41 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
     return w_store, U_store, info
 
 
+def GPT_SGLDERMw(phi, y, signal_var, I, r, Q, m, epsw, burnin, maxepoch, param_seed=0,
+                 w_init=None, U_init=None, max_steps=None, record=False):
+    """GPT_SGLD.jl:1065-1118 — SGLD on w alone, U fixed at its uniform Stiefel draw (σ_w = 1).
+    Same init, permutations and w-noise stream as GPTregression; returns (w_store, U, info)
+    with w_store (Q, maxepoch·numbatches)."""
+    phi = np.asarray(phi, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64).ravel()
+    n, D, N = phi.shape
+    numbatches = -(-N // m)
+    if w_init is None or U_init is None:
+        w0, U0 = init_state(n, r, D, Q, param_seed, True, 1.0)
+    w = np.array(w0 if w_init is None else w_init, dtype=np.float64)
+    U = np.array(U0 if U_init is None else U_init, dtype=np.float64, order="F")
+    w_store = np.zeros((Q, maxepoch * numbatches), order="F")
+    info = dict(status=0, gradw_norm=[])
+    order = np.arange(N)
+    step = 0
+    for epoch in range(1, burnin + maxepoch + 1):
+        order = order[px.randperm(N, param_seed, epoch - 1)]
+        for batch in range(1, numbatches + 1):
+            if max_steps is not None and step >= max_steps:
+                return w_store, U, info
+            idx = order[m * (batch - 1): min(m * batch, N)]
+            V = computeV(phidotU(U, phi[:, :, idx]), I)                       # :1095-1098
+            fhat = V.T @ w                                                      # :1101
+            gradw = (N / len(idx)) * V @ (y[idx] - fhat) / signal_var - w      # :1104
+            if record:
+                info["gradw_norm"].append(np.linalg.norm(gradw))
+            w = w + epsw * gradw / 2 + math.sqrt(epsw) * px.normals(Q, param_seed, step, px.W_NOISE, 0)
+            if epoch > burnin:
+                w_store[:, (epoch - burnin - 1) * numbatches + batch - 1] = w
+            step += 1
+    return w_store, U, info
+
+
 RMS_LAMBDA = 1e-5   # GPT_SGLD.jl:1146 smoothing constant
 
 

@@ -173,6 +173,29 @@ def test_rmsprop_trajectory_matches_oracle(name):
     assert rel(dg[1:], np.array(info["gradU_norm"]).T) < 1e-9
 
 
+WONLY_CASES = {
+    # name: (n, D, N, r, Q, m, burnin, maxepoch, epsw)
+    "small": (16, 3, 40, 2, 6, 8, 1, 2, 1e-4),
+    "ragged": (24, 4, 37, 3, 10, 8, 0, 3, 1e-4),
+    "kin40k_shape": (500, 8, 150, 5, 200, 50, 1, 1, 1e-5),
+}
+
+
+@pytest.mark.parametrize("name", list(WONLY_CASES))
+def test_sgldermw_matches_oracle(name):
+    """GPT_SGLDERMw (GPT_SGLD.jl:1065-1118): w-only SGLD with the Stiefel U held fixed."""
+    n, D, N, r, Q, m, burnin, maxepoch, eps = WONLY_CASES[name]
+    p = make_problem(n, D, N, r, Q, seed=17)
+    sv, seed = 0.05, 31
+    ws, U, gn = G().GPT_SGLDERMw(p["phi"], p["y"], sv, p["I"], r, Q, m, eps, burnin, maxepoch, seed,
+                                 diag=True)
+    wo, Uo, info = R.GPT_SGLDERMw(p["phi"], p["y"], sv, p["I"], r, Q, m, eps, burnin, maxepoch,
+                                  seed, record=True)
+    assert rel(U, Uo) < 1e-14
+    assert rel(ws, wo) < 1e-9, rel(ws, wo)
+    assert rel(gn, np.array(info["gradw_norm"])) < 1e-9
+
+
 def test_sgldERM_generation_a_mapping():
     n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
     p = make_problem(n, D, N, r, Q, seed=4)

@@ -227,3 +227,20 @@ def test_tgp_draws_and_conditional_mean():
     mu = np.linalg.solve(M, V @ y / sigma ** 2)
     z = np.linalg.cholesky(M).T @ (W[:, 0] - mu)
     assert np.abs(z - px.normals(q, 4, 0, px.TGP_W_NOISE, 0)).max() < 1e-9
+
+
+def test_sgldermw_oracle_keeps_U_and_matches_first_step():
+    rng = np.random.default_rng(8)
+    n, D, N, r, Q, m = 6, 2, 20, 2, 3, 10
+    phi = rng.standard_normal((n, D, N))
+    y = rng.standard_normal(N)
+    I = R.samplenz(r, D, Q, 2)
+    ws, U, info = R.GPT_SGLDERMw(phi, y, 0.3, I, r, Q, m, 1e-3, 0, 1, 5, record=True)
+    w0, U0 = R.init_state(n, r, D, Q, 5, True, 1.0)
+    assert np.array_equal(U, U0)
+    idx = np.arange(N)[px.randperm(N, 5, 0)][:m]
+    V = R.computeV(R.phidotU(U0, phi[:, :, idx]), I)
+    g = (N / m) * V @ (y[idx] - V.T @ w0) / 0.3 - w0
+    w1 = w0 + 1e-3 * g / 2 + math.sqrt(1e-3) * px.normals(Q, 5, 0, px.W_NOISE, 0)
+    assert np.allclose(ws[:, 0], w1, rtol=0, atol=1e-13)
+    assert abs(info["gradw_norm"][0] - np.linalg.norm(g)) < 1e-10 * np.linalg.norm(g)
