@@ -15,6 +15,7 @@ Same function names, argument meaning, return values and error behaviour as the 
     GPT_SGLDERMw(phi, y, signal_var, I, r, Q, m, epsw, burnin, maxepoch)  GPT_SGLD.jl:1065
     pred(w, U, I, phitest)                                    GPT_SGLD.jl:233
     RMSE(w_store, U_store, I, phitest, ytest)                 GPT_SGLD_p.jl:124
+    pred_mean_x(w_store, U_store, I, Xtest, ytest, ls, σ, scale, Z, b)  fused feature + pred
     GPNT_SGLD(phi, y, signal_var, sigma_theta, m, eps_theta, decay_rate, burnin, maxepoch,
               param_seed)                                     GPT_SGLD.jl:809
     datawhitening(X), proj, geod are not on the device path (host prep / inside the kernel).
@@ -311,6 +312,34 @@ def pred_mean(w_store, U_store, I, phitest, ytest, scale=1.0):
     check(lib().gpt_pred_mean(_ptr(w_store), _ptr(U_store), _ptr(I, P_I32), _ptr(phitest), _ptr(yt),
                               n, D, Nt, r, Q, S, float(scale), _ptr(mean), C.byref(rm)))
     return mean, rm.value
+
+
+def pred_mean_x(w_store, U_store, I, Xtest, ytest, length_scale, sigma_RBF, phi_scale, Z, b,
+                scale=1.0):
+    """pred_mean with the test features formed inside the prediction kernel from Xtest (no
+    n·D·Ntest phitest array; same doubles as ``feature(Xtest, length_scale, sigma_RBF,
+    phi_scale, Z, b)``).  Returns (meanfhat, rmse, per-sample rmse) — the last is the
+    ``testRMSE`` curve of kin40kExperiment.jl:78-83 when the samples are the epoch ends."""
+    X = _f64(Xtest)
+    Nt, D = X.shape
+    Z = _f64(Z)
+    n = Z.shape[0]
+    b = _f64(np.asarray(b, dtype=np.float64).reshape((n, D), order="F"))
+    ls = _f64(np.atleast_1d(length_scale))
+    w_store = _f64(w_store)
+    U_store = _f64(U_store)
+    Q, S = w_store.shape
+    r = U_store.shape[1]
+    I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+    yt = _f64(np.asarray(ytest, dtype=np.float64).ravel())
+    mean = np.empty(Nt)
+    srm = np.empty(S)
+    rm = C.c_double(0.0)
+    check(lib().gpt_pred_mean_x(_ptr(w_store), _ptr(U_store), _ptr(I, P_I32), _ptr(X), _ptr(yt), Nt,
+                                D, _ptr(ls), ls.size, float(sigma_RBF), float(phi_scale), _ptr(Z),
+                                _ptr(b), n, r, Q, S, float(scale), _ptr(mean), C.byref(rm),
+                                _ptr(srm)))
+    return mean, rm.value, srm
 
 
 def RMSE(w_store, U_store, I, phitest, ytest):

@@ -872,6 +872,66 @@ extern "C" int gpt_pred_mean(const double* w_store, const double* U_store, const
                    mean_out, rmse_out);
 }
 
+extern "C" int gpt_pred_mean_x(const double* w_store, const double* U_store, const int32_t* I,
+                               const double* Xtest, const double* ytest, int64_t Ntest, int64_t D,
+                               const double* length_scale, int64_t ls_len, double sigma_rbf,
+                               double phi_scale, const double* Z, const double* b, int64_t n,
+                               int64_t r, int64_t Q, int64_t S, double scale, double* mean_out,
+                               double* rmse_out, double* sample_rmse_out) {
+  if (!w_store || !U_store || !I || !Xtest || !ytest || !length_scale || !Z || !b || S < 1) {
+    set_error("bad pred_mean_x arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  if (ls_len != 1 && ls_len != D) {
+    set_error("dimensions of X and length_scale do not match"); return GPT_ERR_BAD_DIMS;
+  }
+  if (!valid_pred(n, D, Ntest, r, Q)) return GPT_ERR_BAD_DIMS;
+  if (pred_x_lds_bytes((int)n, (int)D, (int)r, (int)Q) > 160 * 1024) {
+    set_error("pred LDS too large"); return GPT_ERR_BAD_DIMS;
+  }
+  std::vector<int32_t> I0((size_t)Q * D);
+  for (size_t x = 0; x < I0.size(); ++x) {
+    if (I[x] < 1 || I[x] > r) { set_error("I entries must be in 1..r"); return GPT_ERR_BAD_DIMS; }
+    I0[x] = I[x] - 1;
+  }
+  std::vector<double> lsv(D);
+  for (int64_t k = 0; k < D; ++k) lsv[k] = length_scale[ls_len == 1 ? 0 : k];
+  const double c = phi_scale * std::pow(sigma_rbf, 1.0 / (double)D) * std::sqrt(2.0 / (double)n);
+  DevMem dw, dU, dI, dX, dls, dZ, db, df, dy, dmean, dsse;
+  HIPCHK(dw.alloc(8 * (size_t)Q * S));
+  HIPCHK(dU.alloc(8 * (size_t)n * r * D * S));
+  HIPCHK(dI.alloc(4 * I0.size()));
+  HIPCHK(dX.alloc(8 * (size_t)Ntest * D));
+  HIPCHK(dls.alloc(8 * (size_t)D));
+  HIPCHK(dZ.alloc(8 * (size_t)n * D));
+  HIPCHK(db.alloc(8 * (size_t)n * D));
+  HIPCHK(df.alloc(8 * (size_t)Ntest * S));
+  HIPCHK(dy.alloc(8 * (size_t)Ntest));
+  HIPCHK(dmean.alloc(8 * (size_t)Ntest));
+  HIPCHK(dsse.alloc(8 * (size_t)(S + 1)));
+  HIPCHK(hipMemcpy(dw.p, w_store, 8 * (size_t)Q * S, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dU.p, U_store, 8 * (size_t)n * r * D * S, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dI.p, I0.data(), 4 * I0.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dX.p, Xtest, 8 * (size_t)Ntest * D, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dls.p, lsv.data(), 8 * (size_t)D, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dZ.p, Z, 8 * (size_t)n * D, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(db.p, b, 8 * (size_t)n * D, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy.p, ytest, 8 * (size_t)Ntest, hipMemcpyHostToDevice));
+  hipError_t e = launch_pred_x(dw.as<double>(), dU.as<double>(), dI.as<int32_t>(), dX.as<double>(),
+                               dls.as<double>(), dZ.as<double>(), db.as<double>(), c, (int)n, (int)D,
+                               Ntest, (int)r, (int)Q, (int)S, df.as<double>(), nullptr);
+  if (e != hipSuccess) return hip_fail(e, "pred_x kernel");
+  e = launch_mean_rmse(df.as<double>(), dy.as<double>(), Ntest, (int)S, dmean.as<double>(),
+                       dsse.as<double>(), nullptr);
+  if (e != hipSuccess) return hip_fail(e, "mean/sse kernel");
+  std::vector<double> sse((size_t)S + 1);
+  HIPCHK(hipMemcpy(sse.data(), dsse.p, 8 * sse.size(), hipMemcpyDeviceToHost));
+  if (mean_out) HIPCHK(hipMemcpy(mean_out, dmean.p, 8 * (size_t)Ntest, hipMemcpyDeviceToHost));
+  if (rmse_out) *rmse_out = scale * std::sqrt(sse[0] / (double)Ntest);
+  if (sample_rmse_out)
+    for (int64_t z = 0; z < S; ++z) sample_rmse_out[z] = scale * std::sqrt(sse[1 + z] / (double)Ntest);
+  return GPT_OK;
+}
+
 extern "C" int gpt_gpnt_sgld(const double* phi, const double* y, int64_t n, int64_t N,
                              double signal_var, double sigma_theta, int64_t m, double eps_theta,
                              double decay_rate, int64_t burnin, int64_t maxepoch, uint64_t seed,

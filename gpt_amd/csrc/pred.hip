@@ -48,6 +48,106 @@ __global__ __launch_bounds__(kNT) void pred_kernel(const double* __restrict__ w,
   });
 }
 
+size_t pred_lds_bytes(int n, int D, int r, int Q);
+
+// phidotU_tile with the feature rows formed on the fly, in feature_kernel's arithmetic (the same
+// doubles as a materialised phi): temp[l][i] = Σ_j c·cos(X[i0+i, k]·zt[j] + bj[j]) · U_l[l][j],
+// zt = Z[:,k]·(1/ls[k]) and bj = b[:,k] staged (zero-padded to NP) in LDS.
+template <int R, class Out>
+__device__ __forceinline__ void featdotU_tile(const double* __restrict__ Xk, double c,
+                                              const double* zt, const double* bj, long long rowbase,
+                                              int Bt, int NP, int NS, const double* U_l, Out out) {
+  using Cf = RCfg<R>;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+  constexpr int SH = 6 - Butterfly<Cf::NV>::P;
+  for (int base = 0; base < Bt; base += kNW * Cf::ICH) {
+    double v[Cf::NV];
+#pragma unroll
+    for (int u = 0; u < Cf::NV; ++u) v[u] = 0.0;
+    double xv[Cf::ICH];
+#pragma unroll
+    for (int ii = 0; ii < Cf::ICH; ++ii)
+      xv[ii] = gptr(Xk)[rowbase + min(base + wv + kNW * ii, Bt - 1)];
+    const int JS = NP >> 6;
+#pragma unroll 2
+    for (int s2 = 0; s2 < JS; ++s2) {
+      const int j = lane + 64 * s2;
+      const double z = zt[j], bb = bj[j];
+      double u[R];
+#pragma unroll
+      for (int l = 0; l < R; ++l) u[l] = U_l[l * NS + j];
+#pragma unroll
+      for (int ii = 0; ii < Cf::ICH; ++ii) {
+        const double p = c * cos(__dadd_rn(__dmul_rn(xv[ii], z), bb));
+#pragma unroll
+        for (int l = 0; l < R; ++l) v[ii * R + l] = fma(p, u[l], v[ii * R + l]);
+      }
+    }
+    Butterfly<Cf::NV>::run(v, lane);
+    const int vi = lane >> SH;
+    if ((lane & ((1 << SH) - 1)) == 0 && vi < Cf::NVR) {
+      const int ii = vi / R, l = vi - (vi / R) * R;
+      const int i = base + wv + kNW * ii;
+      if (i < Bt) out(l, i, v[0]);
+    }
+  }
+}
+
+// pred_kernel over features formed from Xtest (N × D column-major) instead of a stored phitest.
+template <int R>
+__global__ __launch_bounds__(kNT) void pred_x_kernel(const double* __restrict__ w,
+                                                     const double* __restrict__ U,
+                                                     const int32_t* __restrict__ I0,
+                                                     const double* __restrict__ X,
+                                                     const double* __restrict__ ls,
+                                                     const double* __restrict__ Z,
+                                                     const double* __restrict__ bfe, double c,
+                                                     int n, int D, long long Ntest, int Q,
+                                                     double* __restrict__ fhat) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int MP = 65;
+  const int NP = ((n + 63) / 64) * 64, NS = NP + 1;
+  size_t o = 0;
+  double* temp_l = (double*)(smem + o); o = al16(o + 8 * (size_t)D * R * MP);
+  int* I_l = (int*)(smem + o);          o = al16(o + 4 * (size_t)Q * D);
+  double* w_l = (double*)(smem + o);    o = al16(o + 8 * (size_t)Q);
+  double* zt_l = (double*)(smem + o);   o = al16(o + 8 * (size_t)NP);
+  double* bj_l = (double*)(smem + o);   o = al16(o + 8 * (size_t)NP);
+  double* U_l = (double*)(smem + o);
+  const int tid = threadIdx.x;
+  const int s = blockIdx.y;
+  const long long i0 = (long long)blockIdx.x * 64;
+  const int Bt = (int)min((long long)64, Ntest - i0);
+  const double* ws = w + (size_t)s * Q;
+  const double* Us = U + (size_t)s * n * R * D;
+  for (int x = tid; x < Q * D; x += kNT) I_l[x] = I0[x];
+  for (int q = tid; q < Q; q += kNT) w_l[q] = ws[q];
+  for (int kk = 0; kk < D; ++kk) {
+    __syncthreads();
+    const double* Uk = Us + (size_t)n * R * kk;
+    for (int x = tid; x < R * NP; x += kNT) {
+      const int l = x / NP, j = x - l * NP;
+      U_l[l * NS + j] = j < n ? Uk[j + (size_t)n * l] : 0.0;
+    }
+    const double ils = 1.0 / ls[kk];
+    for (int j = tid; j < NP; j += kNT) {
+      zt_l[j] = j < n ? __dmul_rn(Z[j + (size_t)n * kk], ils) : 0.0;
+      bj_l[j] = j < n ? bfe[j + (size_t)n * kk] : 0.0;
+    }
+    __syncthreads();
+    featdotU_tile<R>(X + (size_t)Ntest * kk, c, zt_l, bj_l, i0, Bt, NP, NS, U_l,
+                     [&](int l, int i, double v) { temp_l[(kk * R + l) * MP + i] = v; });
+  }
+  __syncthreads();
+  vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, I_l, w_l, Q, D, 0, Bt, [&](int comp, int i, double v) {
+    if (comp == 0) fhat[(size_t)s * Ntest + i0 + i] = v;
+  });
+}
+
+size_t pred_x_lds_bytes(int n, int D, int r, int Q) {
+  return pred_lds_bytes(n, D, r, Q) + 2 * al16(8 * (size_t)(((n + 63) / 64) * 64));
+}
+
 size_t pred_lds_bytes(int n, int D, int r, int Q) {
   size_t o = 0;
   o = al16(o + 8 * (size_t)D * r * 65);
@@ -108,6 +208,33 @@ hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, cons
     }                                                                                        \
     hipLaunchKernelGGL(pred_kernel<RR>, grid, dim3(kNT), lds, st, w, U, I0, phitest, n, D,   \
                        Ntest, Q, fhat);                                                      \
+  } break;
+    GPT_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_pred_x(const double* w, const double* U, const int32_t* I0, const double* X,
+                         const double* ls, const double* Z, const double* bfe, double c, int n,
+                         int D, long long Ntest, int r, int Q, int S, double* fhat,
+                         hipStream_t st) {
+  if (Ntest <= 0 || S <= 0) return hipSuccess;
+  const size_t lds = pred_x_lds_bytes(n, D, r, Q);
+  dim3 grid((unsigned)((Ntest + 63) / 64), S);
+  switch (r) {
+#define CASE(RR)                                                                             \
+  case RR: {                                                                                 \
+    static bool attr = false;                                                                \
+    if (!attr) {                                                                             \
+      hipError_t e = hipFuncSetAttribute((const void*)pred_x_kernel<RR>,                      \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      if (e != hipSuccess) return e;                                                         \
+      attr = true;                                                                           \
+    }                                                                                        \
+    hipLaunchKernelGGL(pred_x_kernel<RR>, grid, dim3(kNT), lds, st, w, U, I0, X, ls, Z, bfe, c, \
+                       n, D, Ntest, Q, fhat);                                                \
   } break;
     GPT_RANKS(CASE)
 #undef CASE

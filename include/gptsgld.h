@@ -154,6 +154,17 @@ int gpt_pred_mean(const double* w_store, const double* U_store, const int32_t* I
                   int64_t Ntest, int64_t r, int64_t Q, int64_t S, double scale,
                   double* mean_out, double* rmse_out);
 
+/* Fused feature + posterior-mean prediction (§8(f) per-epoch evaluation, kin40kExperiment.jl:78-87):
+ * the test features phi = feature(Xtest, length_scale, sigma_rbf, phi_scale, Z, b) are formed
+ * inside the prediction kernel (no n*D*Ntest phitest array; the same doubles gpt_feature makes).
+ * Xtest (Ntest, D) column-major.  mean_out (Ntest) and *rmse_out as gpt_pred_mean;
+ * sample_rmse_out (S, optional) = scale*||ytest - pred(sample s)||/sqrt(Ntest), the testRMSE curve. */
+int gpt_pred_mean_x(const double* w_store, const double* U_store, const int32_t* I,
+                    const double* Xtest, const double* ytest, int64_t Ntest, int64_t D,
+                    const double* length_scale, int64_t ls_len, double sigma_rbf, double phi_scale,
+                    const double* Z, const double* b, int64_t n, int64_t r, int64_t Q, int64_t S,
+                    double scale, double* mean_out, double* rmse_out, double* sample_rmse_out);
+
 /* ---- full-theta model (config 1) ----------------------------------------------------- */
 /* GPNT_SGLD(phi,y,signal_var,sigma_theta,m,eps_theta,decay_rate,burnin,maxepoch,param_seed)
  * GPT_SGLD.jl:809-847 -> theta_store (n, (maxepoch+burnin)*numbatches) */

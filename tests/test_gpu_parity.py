@@ -173,6 +173,29 @@ def test_rmsprop_trajectory_matches_oracle(name):
     assert rel(dg[1:], np.array(info["gradU_norm"]).T) < 1e-9
 
 
+def test_pred_mean_x_fused_features():
+    """Fused feature+pred (§8(f) per-epoch evaluation) equals pred_mean over materialised
+    features, and the per-sample RMSE curve matches the oracle."""
+    rng = np.random.default_rng(21)
+    n, D, Nt, r, Q, S = 40, 4, 333, 3, 20, 3
+    X = rng.standard_normal((Nt, D)); Z = rng.standard_normal((n, D)); b = 2 * np.pi * rng.random((n, D))
+    ls = 1 + 0.2 * rng.standard_normal(D)
+    I = R.samplenz(r, D, Q, 3)
+    ws = rng.standard_normal((Q, S))
+    Us = np.stack([R.init_state(n, r, D, Q, 10 + s)[1] for s in range(S)], axis=3)
+    yt = rng.standard_normal(Nt)
+    mean, rm, srm = G().pred_mean_x(ws, Us.reshape((n, r, D * S), order="F"), I, X, yt, ls, 1.1,
+                                    2.0, Z, b, scale=1.7)
+    phi = G().feature(X, ls, 1.1, 2.0, Z, b)
+    mean2, rm2 = G().pred_mean(ws, Us.reshape((n, r, D * S), order="F"), I, phi, yt, scale=1.7)
+    assert rel(mean, mean2) < 1e-15 and abs(rm - rm2) <= 1e-15 * rm2
+    phio = R.feature(X, ls, 1.1, 2.0, Z, b)
+    f = np.stack([R.pred(ws[:, s], Us[..., s], I, phio) for s in range(S)])
+    assert rel(mean, f.mean(axis=0)) < 1e-12
+    want = 1.7 * np.sqrt(((f - yt) ** 2).mean(axis=1))
+    assert np.abs(srm - want).max() <= 1e-12 * want.max()
+
+
 WONLY_CASES = {
     # name: (n, D, N, r, Q, m, burnin, maxepoch, epsw)
     "small": (16, 3, 40, 2, 6, 8, 1, 2, 1e-4),
