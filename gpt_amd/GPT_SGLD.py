@@ -13,6 +13,8 @@ Same function names, argument meaning, return values and error behaviour as the 
                   langevin, stiefel)                          GPT_SGLD.jl:345
     GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch)  GPT_SGLD_p.jl:146
     GPT_SGLDERMw(phi, y, signal_var, I, r, Q, m, epsw, burnin, maxepoch)  GPT_SGLD.jl:1065
+    GPTclassification(phi, y, I, r, Q, m, epsw, epsU, burnin, maxepoch[, param_seed];
+                      langevin, stiefel)                      GPT_SGLD.jl:452
     pred(w, U, I, phitest)                                    GPT_SGLD.jl:233
     RMSE(w_store, U_store, I, phitest, ytest)                 GPT_SGLD_p.jl:124
     pred_mean_x(w_store, U_store, I, Xtest, ytest, ls, σ, scale, Z, b)  fused feature + pred
@@ -271,6 +273,40 @@ def GPT_SGLDERMw(phi, y, signal_var, I, r, Q, m, epsw, burnin, maxepoch, param_s
                                _ptr(Ui) if Ui is not None else None, _ptr(w_store), _ptr(U),
                                _ptr(dg) if diag else None))
     return (w_store, U, dg[0].copy()) if diag else (w_store, U)
+
+
+def GPTclassification(phi, y, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0,
+                      langevin=True, stiefel=True, w_init=None, U_init=None, diag=False):
+    """Softmax tensor-GP classifier (GPT_SGLD.jl:452-680), labels y in 1..C.  Returns
+    (w_store (Q, C, T), U_store (n, r, D, C, T)) [, diag (1+D, steps, C)]; on the geodesic NaN
+    bail-out prints the reference's message and returns zeros."""
+    phi = _f64(phi)
+    n, D, N = phi.shape
+    y = _f64(np.asarray(y, dtype=np.float64).ravel())
+    if y.size != N:
+        raise ValueError("phi and y disagree on N")
+    ncls = int(y.max() - y.min() + 1)
+    I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+    if I.shape != (Q, D):
+        raise ValueError("I must be (Q, D)")
+    cfg = make_config(n, D, N, r, Q, m, epsw, epsU, 1.0, 1.0, burnin, maxepoch, param_seed,
+                      langevin, stiefel, 1, 0)
+    nb = -(-N // m)
+    T = maxepoch * nb
+    w_store = np.zeros((Q, ncls, T), order="F")
+    U_store = np.zeros((n, r, D, ncls, T), order="F")
+    dg = np.zeros((1 + D, (burnin + maxepoch) * nb, ncls), order="F") if diag else None
+    wi = _f64(w_init) if w_init is not None else None
+    Ui = _f64(U_init) if U_init is not None else None
+    code = lib().gpt_sgld_classification(C.byref(cfg), _ptr(phi), _ptr(y), _ptr(I, P_I32),
+                                         _ptr(wi) if wi is not None else None,
+                                         _ptr(Ui) if Ui is not None else None, _ptr(w_store),
+                                         _ptr(U_store), _ptr(dg) if diag else None)
+    if code == _lib.GPT_ERR_NAN_GEODESIC:
+        print("Get NaN when moving along Geodesic. Try smaller epsU")
+    else:
+        check(code)
+    return (w_store, U_store, dg) if diag else (w_store, U_store)
 
 
 def GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0, **kw):

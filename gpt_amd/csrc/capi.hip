@@ -84,16 +84,18 @@ static void jacobi_eig(int r, std::vector<double>& A, std::vector<double>& V,
 }
 
 // GPT_SGLD.jl:357-369: w = σ_w·randn(Q); U_k = Zᵀ(ZZᵀ)^(-1/2), Z = randn(r,n)  (or randn/√n).
+// Class cls of GPTclassification (GPT_SGLD.jl:463-477) draws w on (W_INIT, cls) and U_k on
+// (U_INIT, k + D·cls), and its non-Stiefel U is randn unscaled (cls_init).
 void host_init_state(int n, int r, int D, int Q, uint64_t seed, bool stiefel, double sigma_w,
-                     double* w, double* U) {
-  for (int q = 0; q < Q; ++q) w[q] = sigma_w * host_normal(seed, q, 0, kWInit, 0);
+                     double* w, double* U, int cls, bool cls_init) {
+  for (int q = 0; q < Q; ++q) w[q] = sigma_w * host_normal(seed, q, 0, kWInit, (uint32_t)cls);
   std::vector<double> Z((size_t)r * n), G, Vv, ev;
   for (int k = 0; k < D; ++k) {
-    for (int e = 0; e < r * n; ++e) Z[e] = host_normal(seed, e, 0, kUInit, k);  // Z[a + r*j]
+    for (int e = 0; e < r * n; ++e) Z[e] = host_normal(seed, e, 0, kUInit, (uint32_t)(k + D * cls));  // Z[a + r*j]
     double* Uk = U + (size_t)n * r * k;
     if (!stiefel) {
       for (int j = 0; j < n; ++j)
-        for (int a = 0; a < r; ++a) Uk[j + (size_t)n * a] = Z[a + (size_t)r * j] / std::sqrt((double)n);
+        for (int a = 0; a < r; ++a) Uk[j + (size_t)n * a] = cls_init ? Z[a + (size_t)r * j] : Z[a + (size_t)r * j] / std::sqrt((double)n);
       continue;
     }
     G.assign((size_t)r * r, 0.0);
@@ -212,7 +214,7 @@ static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t 
   const bool grid_ok =
       step_layout((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m).bytes <= 160 * 1024;
   int want = -1;
-  if (flags & (4 | 16)) want = kEngineGrid;
+  if (flags & (4 | 16 | 32)) want = kEngineGrid;
   else if (flags & 8) want = kEngineChain;
   else if (const char* ev = std::getenv("GPTSGLD_ENGINE")) {
     if (!std::strcmp(ev, "grid")) want = kEngineGrid;
@@ -258,6 +260,9 @@ extern "C" int gpt_device_count(void) {
 }
 
 static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t_local) {
+  if (P.ncls)
+    return launch_step_cls(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
+                           t_local, s->stream);
   if (P.wonly)
     return launch_step_wonly(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
                              t_local, s->stream);
@@ -351,6 +356,7 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   P.stamps = nullptr;
   P.rms = 0; P.rms_eps = 0.0; P.rms_alpha = 0.0;
   P.wonly = (store_flags & 16) ? 1 : 0;
+  P.ncls = (store_flags & 32) ? nchains : 0;
   HIPCHK(s->tbase.alloc(sizeof(long long)));
   HIPCHK(hipMemset(s->tbase.p, 0, sizeof(long long)));
   HIPCHK(s->status.alloc(sizeof(int32_t) * nchains));
@@ -421,6 +427,25 @@ extern "C" int gpt_sgld_session_set_hyper(gpt_sgld_session* s, int32_t chain, do
   return GPT_OK;
 }
 
+// Per-chain zeroed gw (Q) | gU (n·r·D) | res (m) buffers of the RMSprop and classification steps.
+static int session_alloc_aux(gpt_sgld_session* s) {
+  const StepParams& P = s->P;
+  const size_t bq = 8 * (size_t)P.Q, bu = 8 * (size_t)P.n * P.r * P.D, br = 8 * (size_t)P.m;
+  for (int c = 0; c < s->nchains; ++c) {
+    std::unique_ptr<DevMem> mem(new DevMem());
+    HIPCHK(mem->alloc(bq + bu + br));
+    HIPCHK(hipMemset(mem->p, 0, bq + bu + br));
+    ChainDesc& C = s->chains_h[c];
+    C.gw = mem->as<double>();
+    C.gU = C.gw + P.Q;
+    C.res = C.gU + (size_t)P.n * P.r * P.D;
+    s->chain_mem.push_back(std::move(mem));
+  }
+  HIPCHK(hipMemcpy(s->chains_d.p, s->chains_h.data(), sizeof(ChainDesc) * s->nchains,
+                   hipMemcpyHostToDevice));
+  return GPT_OK;
+}
+
 extern "C" int gpt_sgld_session_set_rmsprop(gpt_sgld_session* s, double epsilon, double alpha) {
   if (!s) { set_error("null session"); return GPT_ERR_BAD_DIMS; }
   if (s->engine != kEngineGrid) {
@@ -435,20 +460,8 @@ extern "C" int gpt_sgld_session_set_rmsprop(gpt_sgld_session* s, double epsilon,
   if (!(epsilon > 0) || !(alpha >= 0 && alpha < 1)) {
     set_error("RMSprop needs epsilon > 0 and 0 <= alpha < 1"); return GPT_ERR_BAD_DIMS;
   }
-  const StepParams& P = s->P;
-  const size_t bq = 8 * (size_t)P.Q, bu = 8 * (size_t)P.n * P.r * P.D, br = 8 * (size_t)P.m;
-  for (int c = 0; c < s->nchains; ++c) {
-    std::unique_ptr<DevMem> mem(new DevMem());
-    HIPCHK(mem->alloc(bq + bu + br));
-    HIPCHK(hipMemset(mem->p, 0, bq + bu + br));    // moving averages start at 0 (:1143-1144)
-    ChainDesc& C = s->chains_h[c];
-    C.gw = mem->as<double>();
-    C.gU = C.gw + P.Q;
-    C.res = C.gU + (size_t)P.n * P.r * P.D;
-    s->chain_mem.push_back(std::move(mem));
-  }
-  HIPCHK(hipMemcpy(s->chains_d.p, s->chains_h.data(), sizeof(ChainDesc) * s->nchains,
-                   hipMemcpyHostToDevice));
+  const int rc = session_alloc_aux(s);     // moving averages start at 0 (:1143-1144)
+  if (rc != GPT_OK) return rc;
   s->P.rms = 1; s->P.rms_eps = epsilon; s->P.rms_alpha = alpha;
   return GPT_OK;
 }
@@ -694,6 +707,80 @@ extern "C" int gpt_sgld_wonly(const gpt_sgld_config* cfg, const double* phi, con
     return GPT_ERR_BAD_DIMS;
   }
   return host_sampler(cfg, phi, y, I, w_init, U_init, w_store, nullptr, diag, 16, 0.0, 0.0, U_out);
+}
+
+extern "C" int gpt_sgld_classification(const gpt_sgld_config* cfg, const double* phi,
+                                       const double* y, const int32_t* I, const double* w_init,
+                                       const double* U_init, double* w_store, double* U_store,
+                                       double* diag) {
+  if (!valid_cfg(cfg)) return GPT_ERR_BAD_DIMS;
+  if (!phi || !y || !I) { set_error("null input"); return GPT_ERR_BAD_DIMS; }
+  const int64_t N = cfg->N, Q = cfg->Q, nur = cfg->n * cfg->r * cfg->D;
+  long long lo = 0, hi = 0;
+  for (int64_t i = 0; i < N; ++i) {
+    const double v = y[i];
+    if (v != std::floor(v)) { set_error("class labels must be integers"); return GPT_ERR_BAD_DIMS; }
+    lo = i ? std::min(lo, (long long)v) : (long long)v;
+    hi = i ? std::max(hi, (long long)v) : (long long)v;
+  }
+  if (lo != 1 || hi > 64) {
+    set_error("class labels must be 1..C (C <= 64): they index the classes (GPT_SGLD.jl:520)");
+    return GPT_ERR_BAD_DIMS;
+  }
+  const int ncls = (int)hi;
+  const size_t nphi = (size_t)cfg->n * cfg->D * N;
+  DevMem dphi, dy;
+  HIPCHK(dphi.alloc(8 * nphi));
+  HIPCHK(dy.alloc(8 * (size_t)N));
+  HIPCHK(hipMemcpy(dphi.p, phi, 8 * nphi, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy.p, y, 8 * (size_t)N, hipMemcpyHostToDevice));
+  std::vector<uint64_t> seeds(ncls, cfg->seed);
+  std::vector<const double*> pp(ncls, dphi.as<double>()), yy(ncls, dy.as<double>());
+  gpt_sgld_session* s = nullptr;
+  const int flags = ((w_store || U_store) ? 1 : 0) | (diag ? 2 : 0) | 32;
+  int rc = gpt_sgld_session_create(cfg, ncls, seeds.data(), pp.data(), yy.data(), I, flags, nullptr, &s);
+  if (rc != GPT_OK) return rc;
+  std::unique_ptr<gpt_sgld_session, void (*)(gpt_sgld_session*)> guard(s, gpt_sgld_session_destroy);
+  rc = session_alloc_aux(s);
+  if (rc != GPT_OK) return rc;
+  std::vector<double> w0((size_t)Q), U0((size_t)nur);
+  for (int c = 0; c < ncls; ++c) {
+    rc = gpt_sgld_session_set_hyper(s, c, cfg->epsw, cfg->epsU, 1.0, 1.0);   // no noise variance
+    if (rc != GPT_OK) return rc;
+    if (w_init && U_init) {
+      rc = session_set_state(s, c, w_init + (size_t)Q * c, U_init + (size_t)nur * c);
+    } else {
+      host_init_state((int)cfg->n, (int)cfg->r, (int)cfg->D, (int)Q, cfg->seed, cfg->stiefel != 0,
+                      1.0, w0.data(), U0.data(), c, true);
+      rc = session_set_state(s, c, w0.data(), U0.data());
+    }
+    if (rc != GPT_OK) return rc;
+  }
+  rc = gpt_sgld_session_run(s, s->total_steps);
+  if (rc != GPT_OK) return rc;
+  const int64_t T = s->nstore, steps = s->total_steps;
+  std::vector<double> wb(w_store ? (size_t)Q * T : 0), Ub(U_store ? (size_t)nur * T : 0),
+      db(diag ? (size_t)(1 + cfg->D) * steps : 0);
+  bool bad = false;
+  for (int c = 0; c < ncls; ++c) {
+    int32_t st = 0;
+    rc = gpt_sgld_session_fetch(s, c, w_store ? wb.data() : nullptr, U_store ? Ub.data() : nullptr,
+                                diag ? db.data() : nullptr, &st);
+    if (rc != GPT_OK) return rc;
+    bad |= st != 0;
+    for (int64_t z = 0; z < T; ++z) {      // (Q, C, T) and (n, r, D, C, T) column-major
+      if (w_store) std::memcpy(w_store + ((size_t)z * ncls + c) * Q, wb.data() + (size_t)z * Q, 8 * Q);
+      if (U_store) std::memcpy(U_store + ((size_t)z * ncls + c) * nur, Ub.data() + (size_t)z * nur, 8 * nur);
+    }
+    if (diag) std::memcpy(diag + (size_t)c * db.size(), db.data(), 8 * db.size());
+  }
+  if (bad) {                               // GPT_SGLD.jl:632-634: zero stores
+    if (w_store) std::memset(w_store, 0, 8 * (size_t)Q * ncls * T);
+    if (U_store) std::memset(U_store, 0, 8 * (size_t)nur * ncls * T);
+    set_error("Get NaN when moving along Geodesic. Try smaller epsU");
+    return GPT_ERR_NAN_GEODESIC;
+  }
+  return GPT_OK;
 }
 
 extern "C" int gpt_samplenz(int64_t r, int64_t D, int64_t Q, uint64_t seed, int32_t* I_out) {

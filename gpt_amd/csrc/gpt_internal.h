@@ -52,6 +52,8 @@ struct StepParams {
   long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
   int rms;                        // 1: GPT_SGLDERM_RMSprop steps (grid engine, two launches)
   int wonly;                      // 1: GPT_SGLDERMw steps (w alone, U fixed; grid engine)
+  int ncls;                       // >= 2: GPTclassification, chains are the classes of one
+                                  // model (grid engine; ChainDesc.res = class fhat, .gU = gradU)
   double rms_eps, rms_alpha;      // its epsilon and moving-average coefficient
 };
 constexpr int kStamps = 16;       // stamp slots per block
@@ -128,6 +130,8 @@ hipError_t launch_step(const StepParams& P, const ChainDesc* chains, int nchains
 // RMSprop step = w phase (one workgroup per chain) then U phase (D workgroups per chain)
 hipError_t launch_step_wonly(const StepParams& P, const ChainDesc* chains, int nchains,
                              const long long* tbase, int t_local, hipStream_t st);
+hipError_t launch_step_cls(const StepParams& P, const ChainDesc* chains, int nchains,
+                           const long long* tbase, int t_local, hipStream_t st);
 hipError_t launch_step_rms(const StepParams& P, const ChainDesc* chains, int nchains,
                            const long long* tbase, int t_local, hipStream_t st);
 hipError_t launch_advance(long long* tbase, long long by, hipStream_t st);
@@ -165,7 +169,7 @@ hipError_t launch_gpnt(const double* phi, const double* y, const int32_t* order,
 
 // Host-side Philox consumers (init / permutations / samplenz)
 void host_init_state(int n, int r, int D, int Q, uint64_t seed, bool stiefel, double sigma_w,
-                     double* w, double* U);
+                     double* w, double* U, int cls = 0, bool cls_init = false);
 void host_epoch_orders(int N, uint64_t seed, int epochs, int32_t* out);  // E*N cumulative
 
 }  // namespace gpt

@@ -31,7 +31,9 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
                                                         int t_local, int kbase) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const ChainDesc C = chains[blockIdx.y];
-  const int k = blockIdx.x + kbase;     // kbase = D: the RMSprop w phase (one workgroup)
+  // kbase = D: the RMSprop w phase (one workgroup); kbase = D + 1: the class-fhat pass of
+  // GPTclassification (one workgroup per class, before the step launch)
+  const int k = blockIdx.x + kbase;
   const int tid = threadIdx.x, wv = uni(tid >> 6);
   const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
@@ -94,16 +96,35 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   // ---- P1: V, fhat, residual, A[:,k,:] (GPT_SGLD.jl:384-399)
   {
     auto vout = [&](int comp, int i, double v) {
-      if (comp == 0) res_l[i] = y_l[i] - v;
+      if (comp == 0) res_l[i] = P.ncls ? v : y_l[i] - v;      // classification: fhat itself
       else coef_l[(comp - 1) * MP + i] = v;
     };
     if (Bt <= kNW * VCfg<R>::ICV_SMALL)
-      vphase_tile<R, VCfg<R>::ICV_SMALL>(temp_l, MP, IT_l, w_l, Q, D, wblock ? 0 : k, Bt, vout);
+      vphase_tile<R, VCfg<R>::ICV_SMALL>(temp_l, MP, IT_l, w_l, Q, D, k >= D ? 0 : k, Bt, vout);
     else
-      vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, IT_l, w_l, Q, D, wblock ? 0 : k, Bt, vout);
+      vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, IT_l, w_l, Q, D, k >= D ? 0 : k, Bt, vout);
   }
   __syncthreads();
   STAMP(2);
+
+  if (P.ncls) {
+    const int cls = blockIdx.y % P.ncls;
+    if (k == D + 1) {               // class-fhat pass: fhat of this class for its siblings
+      for (int i = tid; i < Bt; i += kNT) gptr_w(C.res)[i] = res_l[i];
+      return;
+    }
+    // softmax residual [y_i = c] − exp(fhat_ic − logsumexp_i fhat_i·) (GPT_SGLD.jl:509-526)
+    const ChainDesc* sib = chains + (blockIdx.y - cls);
+    for (int i = tid; i < Bt; i += kNT) {
+      double u = -INFINITY;
+      for (int c2 = 0; c2 < P.ncls; ++c2) u = fmax(u, gptr(sib[c2].res)[i]);
+      double se = 0.0;
+      for (int c2 = 0; c2 < P.ncls; ++c2) se += exp(gptr(sib[c2].res)[i] - u);
+      const double lse = u + log(se);
+      res_l[i] = ((int)y_l[i] == cls + 1 ? 1.0 : 0.0) - exp(gptr(sib[cls].res)[i] - lse);
+    }
+    __syncthreads();
+  }
 
   const double cN = (double)P.N / (double)Bt;
   const long long post = t - P.burnin_steps;
@@ -171,9 +192,20 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       }
       const double wq = w_l[q];
       const double gradw = cN * g / C.signal_var - wq * inv_sw2;
-      double step = C.epsw * gradw / 2;
-      if (P.langevin) step += sqe * normal_at(C.seed, (uint32_t)q, (uint32_t)t, kWNoise, 0);
-      const double wn = wq + step;
+      double wn;
+      if (P.ncls) {                 // two moves with the same gradient (GPT_SGLD.jl:624, :639-642)
+        const int cls = blockIdx.y % P.ncls;
+        const double w1 = wq + (C.epsw * gradw / 2 +
+                                sqe * normal_at(C.seed, (uint32_t)q, (uint32_t)t, kWNoise, 2 * cls));
+        double step = C.epsw * gradw / 2;
+        if (P.langevin)
+          step += sqe * normal_at(C.seed, (uint32_t)q, (uint32_t)t, kWNoise, 2 * cls + 1);
+        wn = w1 + step;
+      } else {
+        double step = C.epsw * gradw / 2;
+        if (P.langevin) step += sqe * normal_at(C.seed, (uint32_t)q, (uint32_t)t, kWNoise, 0);
+        wn = wq + step;
+      }
       gptr_w(C.w)[(size_t)((t + 1) & 1) * Q + q] = wn;
       if (store && C.w_store) gptr_w(C.w_store)[(size_t)slot * Q + q] = wn;
       gn2 = fma(gradw, gradw, gn2);
@@ -232,12 +264,12 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
         // U-noise contract: ξ[j,l] = element l + RE·j of stream (t, U_NOISE, k), RE = R rounded
         // up to even, so one Box–Muller pair serves (l, l+1) of the same row j.
         constexpr int RE = R + (R & 1);
+        const uint32_t c3 = P.ncls ? (uint32_t)(k + D * 2 * (blockIdx.y % P.ncls)) : (uint32_t)k;
 #pragma unroll
         for (int l = 0; l < R; l += 2) {
           double z0 = 0.0, z1 = 0.0;
-          if (P.langevin)
-            normal_pair(C.seed, (uint32_t)((l + RE * jc) >> 1), (uint32_t)t, kUNoise, (uint32_t)k,
-                        z0, z1);
+          if (P.langevin || P.ncls)
+            normal_pair(C.seed, (uint32_t)((l + RE * jc) >> 1), (uint32_t)t, kUNoise, c3, z0, z1);
           xi[l] = z0;
           if (l + 1 < R) xi[l + 1] = z1;
         }
@@ -264,7 +296,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       for (int l = 0; l < R; ++l) {
         const double G = acc[l] * cU;
         gn2 = fma(G, G, gn2);
-        if (P.stiefel) {
+        if (P.ncls) gptr_w(C.gU)[(size_t)n * R * k + (size_t)n * l + j] = G;   // second move
+        if (P.stiefel || P.ncls) {
           W_l[l * NS + j] = sq * G / 2 + xi[l];                  // :420 drive
         } else {                                                  // :426 / :437
           const double u = U_l[l * NS + j];
@@ -295,7 +328,41 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   __syncthreads();
   STAMP(4);
 
-  if (P.stiefel) {
+  // GPTclassification moves U twice with one gradient: pass 0 is SGLD + Stiefel whatever the
+  // flags (GPT_SGLD.jl:627-636), pass 1 the langevin/stiefel variant from pass 0's U (:643-671)
+  const int npass = P.ncls ? 2 : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+  if (pass == 1) {
+    // pass 0's U is the "old U" of pass 1 (re-read from HBM when it is not kept in LDS)
+    for (int o = tid; o < R * n; o += kNT) {
+      const int l = o / n, j = o - l * n;
+      gptr_w(C.U + (size_t)n * R * k)[o] = U_l[l * NS + j];
+    }
+    const uint32_t c3 = (uint32_t)(k + D * (2 * (blockIdx.y % P.ncls) + 1));
+    constexpr int RE = R + (R & 1);
+    for (int j = tid; j < n; j += kNT) {
+#pragma unroll
+      for (int l = 0; l < R; l += 2) {
+        double z0 = 0.0, z1 = 0.0;
+        if (P.langevin)
+          normal_pair(C.seed, (uint32_t)((l + RE * j) >> 1), (uint32_t)t, kUNoise, c3, z0, z1);
+        const double zz[2] = {z0, z1};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (l + h >= R) break;
+          const double G = gptr(C.gU)[(size_t)n * R * k + (size_t)n * (l + h) + j];
+          if (P.stiefel) {
+            W_l[(l + h) * NS + j] = sq * G / 2 + zz[h];
+          } else {
+            const double u = U_l[(l + h) * NS + j];
+            U_l[(l + h) * NS + j] = u + (C.epsU * (G - n * u) / 2 + sq * zz[h]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (pass == 0 ? (P.stiefel || P.ncls) : P.stiefel) {
     double* Mg = gram;              // r×r   Uᵀ·drive
     double* Ag = gram + R * R;      // r×r   Uᵀ·mom
     double* Sg = gram + 2 * R * R;  // r×r   momᵀ·mom
@@ -387,6 +454,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     __syncthreads();
     STAMP(8);
   }
+  }  // pass
 
   // ---- write U^(k) (and the sample store, GPT_SGLD.jl:441-444)
   {
@@ -521,6 +589,25 @@ hipError_t launch_step_wonly(const StepParams& P, const ChainDesc* chains, int n
                        chains, tbase, t_local);                                               \
     hipLaunchKernelGGL(sgld_step_kernel<RR>, dim3(1, nchains), dim3(kNT), L.bytes, st, P,     \
                        chains, tbase, t_local, P.D);                                          \
+    break;
+    GPT_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// GPTclassification: the class-fhat pass (one workgroup per class) then the step of every class.
+hipError_t launch_step_cls(const StepParams& P, const ChainDesc* chains, int nchains,
+                           const long long* tbase, int t_local, hipStream_t st) {
+  const StepLayout L = step_layout(P.n, P.D, P.r, P.Q, P.m);
+  switch (P.r) {
+#define CASE(RR)                                                                              \
+  case RR:                                                                                    \
+    hipLaunchKernelGGL(sgld_step_kernel<RR>, dim3(1, nchains), dim3(kNT), L.bytes, st, P,     \
+                       chains, tbase, t_local, P.D + 1);                                      \
+    hipLaunchKernelGGL(sgld_step_kernel<RR>, dim3(P.D + 1, nchains), dim3(kNT), L.bytes, st,  \
+                       P, chains, tbase, t_local, 0);                                         \
     break;
     GPT_RANKS(CASE)
 #undef CASE

@@ -96,6 +96,16 @@ int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi, const dou
 int gpt_sgld_wonly(const gpt_sgld_config* cfg, const double* phi, const double* y, const int32_t* I,
                    const double* w_init, const double* U_init, double* w_store, double* U_out,
                    double* diag);
+/* GPTclassification(phi,y,I,r,Q,m,epsw,epsU,burnin,maxepoch,param_seed;langevin,stiefel)
+ * GPT_SGLD.jl:452-680: softmax tensor-GP classifier; y holds labels 1..C (as doubles).  cfg:
+ * signal_var / sigma_w are not used (the model has no noise variance, sigma_w = 1).  Optional
+ * w_init (Q, C) / U_init (n, r, D, C).  w_store (Q, C, maxepoch*numbatches), U_store
+ * (n, r, D, C, ...); diag (1+D, steps, C) per-class gradient norms.  As the reference, w and U
+ * move twice per step with one gradient (an SGLD + Stiefel move, then the langevin/stiefel
+ * variant).  Grid engine (store_flags bit 5 in a session: the chains are the C classes). */
+int gpt_sgld_classification(const gpt_sgld_config* cfg, const double* phi, const double* y,
+                            const int32_t* I, const double* w_init, const double* U_init,
+                            double* w_store, double* U_store, double* diag);
 int gpt_sgld_rmsprop(const gpt_sgld_config* cfg, double epsilon, double alpha, const double* phi,
                      const double* y, const int32_t* I, const double* w_init,
                      const double* U_init, double* w_store, double* U_store, double* diag);

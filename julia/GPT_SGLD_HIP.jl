@@ -9,7 +9,7 @@
 module GPT_SGLD_HIP
 
 export datawhitening, feature, featureNotensor, samplenz, GPTregression, GPT_SGLDERM, pred, RMSE,
-       GPNT_SGLD, GPT_SGLDERM_RMSprop, GPT_SGLDERMw
+       GPNT_SGLD, GPT_SGLDERM_RMSprop, GPT_SGLDERMw, GPTclassification
 
 const LIB = get(ENV, "GPTSGLD_LIB", joinpath(@__DIR__, "..", "gpt_amd", "libgptsgld.so"))
 
@@ -142,6 +142,28 @@ function GPT_SGLDERMw(phi::Array{Float64,3}, y::Array{Float64}, signal_var::Real
                  Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
                 cfg, phi, vec(y), I, C_NULL, C_NULL, w_store, U, C_NULL))
     return w_store, U
+end
+
+# GPT_SGLD.jl:452-680 (labels y in 1..C)
+function GPTclassification(phi::Array{Float64,3}, y::Array, I::Array{Int32,2}, r::Integer, Q::Integer,
+                           m::Integer, epsw::Real, epsU::Real, burnin::Integer, maxepoch::Integer,
+                           param_seed::Integer; langevin=true, stiefel=true)
+    n, D, N = size(phi)
+    C = Int(maximum(y) - minimum(y) + 1)
+    cfg = SGLDConfig(n, D, N, r, Q, m, epsw, epsU, 1.0, 1.0, burnin, maxepoch, param_seed,
+                     Int32(langevin), Int32(stiefel), 1, 0)
+    T = maxepoch * cld(N, m)
+    w_store = Array{Float64}(undef, Q, C, T); U_store = Array{Float64}(undef, n, r, D, C, T)
+    rc = ccall((:gpt_sgld_classification, LIB), Cint,
+               (Ref{SGLDConfig}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64},
+                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+               cfg, phi, Float64.(vec(y)), I, C_NULL, C_NULL, w_store, U_store, C_NULL)
+    if rc == 1
+        println("Get NaN when moving along Geodesic. Try smaller epsU")
+        return zeros(Q, C, T), zeros(n, r, D, C, T)
+    end
+    check(rc)
+    return w_store, U_store
 end
 
 function pred(w::Array{Float64}, U::Array{Float64,3}, I::Array{Int32,2}, phitest::Array{Float64,3})

@@ -413,6 +413,125 @@ def GPT_SGLDERMw(phi, y, signal_var, I, r, Q, m, epsw, burnin, maxepoch, param_s
     return w_store, U, info
 
 
+def init_state_cls(n, r, D, Q, ncls, seed, stiefel=True, sigma_w=1.0):
+    """GPT_SGLD.jl:463-477: w = σ_w·randn(Q, C); U[:,:,k,c] uniform on the Stiefel manifold, or
+    randn(n, r, D, C) (unscaled, unlike GPTregression).  Class c draws its w on (W_INIT, c) and
+    U_k on (U_INIT, k + D·c) — class 0 is GPTregression's init."""
+    w = np.empty((Q, ncls), order="F")
+    U = np.empty((n, r, D, ncls), order="F")
+    for c in range(ncls):
+        w[:, c] = sigma_w * px.normals(Q, seed, 0, px.W_INIT, c)
+        for k in range(D):
+            z = px.normals(r * n, seed, 0, px.U_INIT, k + D * c).reshape((r, n), order="F")
+            U[:, :, k, c] = stiefel_init(z) if stiefel else z.T
+    return w, U
+
+
+def logsumexp(x):
+    """max(x) + log(sum(exp(x - max(x)))) (the logsumexp the reference calls at :513)."""
+    u = np.max(x)
+    return u + math.log(np.sum(np.exp(x - u)))
+
+
+def gradients_res(phi_batch, res, w, U, I, N):
+    """gradw = (N/B)·V·res − w and gradU_k = (N/B)·Ψ_k·res (σ_w = 1, no noise variance): the
+    regression gradients with the residual supplied (GPTclassification's [y_i = c] − p_ic)."""
+    n, D, B = phi_batch.shape
+    r = U.shape[1]
+    temp = phidotU(U, phi_batch)
+    V = computeV(temp, I)
+    gradw = (N / B) * (V @ res) - w
+    A = computeA(computeU_phi(V, temp, I), w, I, r)
+    Psi = computePsi(A, phi_batch)
+    gradU = np.empty((n, r, D))
+    for k in range(D):
+        gradU[:, :, k] = ((N / B) * (Psi[:, :, k] @ res)).reshape((n, r), order="F")
+    return gradw, gradU
+
+
+def GPTclassification(phi, y, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed,
+                      langevin=True, stiefel=True, w_init=None, U_init=None, max_steps=None,
+                      record=False):
+    """GPT_SGLD.jl:452-680: softmax tensor-GP classifier, labels y in 1..C, σ_w = 1.
+
+    Per minibatch: fhat[i,c] = V_cᵀw_c for every class, p_ic = exp(fhat_ic − logsumexp_i),
+    residual [y_i = c] − p_ic, gradw/gradU as gradients_res.  As in the reference, w and U are
+    moved TWICE with the same gradients: an unconditional SGLD + Stiefel-geodesic step (:624-636)
+    and then the step selected by langevin/stiefel (:638-671), the second from the first's U.
+    Noise contract: w of class c pass p on (step, W_NOISE, 2c + p); U_k of class c pass p on
+    (step, U_NOISE, k + D·(2c + p)) with u_noise's layout.  Returns (w_store (Q, C, T),
+    U_store (n, r, D, C, T), info); a NaN in a geodesic returns zeros like :632-634."""
+    phi = np.asarray(phi, dtype=np.float64)
+    yl = np.asarray(y).ravel().astype(np.int64)
+    n, D, N = phi.shape
+    ncls = int(yl.max() - yl.min() + 1)
+    nb = -(-N // m)
+    if w_init is None or U_init is None:
+        w0, U0 = init_state_cls(n, r, D, Q, ncls, param_seed, stiefel, 1.0)
+    w = np.array(w0 if w_init is None else w_init, dtype=np.float64, order="F")
+    U = np.array(U0 if U_init is None else U_init, dtype=np.float64, order="F")
+    T = maxepoch * nb
+    w_store = np.zeros((Q, ncls, T), order="F")
+    U_store = np.zeros((n, r, D, ncls, T), order="F")
+    info = dict(status=0, gradw_norm=[], gradU_norm=[])
+    order = np.arange(N)
+    step = 0
+    sq, sqw = math.sqrt(epsU), math.sqrt(epsw)
+
+    def zeros():
+        info["status"] = 1
+        return np.zeros_like(w_store), np.zeros_like(U_store), info
+
+    for epoch in range(1, burnin + maxepoch + 1):
+        order = order[px.randperm(N, param_seed, epoch - 1)]
+        for batch in range(1, nb + 1):
+            if max_steps is not None and step >= max_steps:
+                return w_store, U_store, info
+            idx = order[m * (batch - 1): min(m * batch, N)]
+            pb, yb = phi[:, :, idx], yl[idx]
+            B = len(idx)
+            fhat = np.stack([computefhat(computeV(phidotU(U[..., c], pb), I), w[:, c])
+                             for c in range(ncls)], axis=1)                    # (B, C) :496-506
+            lse = np.array([logsumexp(fhat[i, :]) for i in range(B)])
+            gw, gU = [], []
+            for c in range(ncls):
+                res = (yb == c + 1).astype(np.float64) - np.exp(fhat[:, c] - lse)
+                a, b = gradients_res(pb, res, w[:, c], U[..., c], I, N)
+                gw.append(a)
+                gU.append(b)
+            if record:
+                info["gradw_norm"].append([np.linalg.norm(g) for g in gw])
+                info["gradU_norm"].append([[np.linalg.norm(gU[c][:, :, k]) for k in range(D)]
+                                           for c in range(ncls)])
+            for p in range(2):
+                for c in range(ncls):
+                    noise = (p == 0 or langevin)
+                    w[:, c] += epsw * gw[c] / 2
+                    if noise:
+                        w[:, c] += sqw * px.normals(Q, param_seed, step, px.W_NOISE, 2 * c + p)
+                for c in range(ncls):
+                    for k in range(D):
+                        xi = u_noise(n, r, param_seed, step, k + D * (2 * c + p))
+                        G = gU[c][:, :, k]
+                        if p == 0 or stiefel:
+                            drive = sq * G / 2 + (xi if (p == 0 or langevin) else 0.0)
+                            Un, ok = geod(U[:, :, k, c], proj(U[:, :, k, c], drive), sq)
+                            if not ok:
+                                return zeros()
+                            U[:, :, k, c] = Un
+                        else:
+                            upd = epsU * (G - n * U[:, :, k, c]) / 2
+                            if langevin:
+                                upd = upd + sq * xi
+                            U[:, :, k, c] = U[:, :, k, c] + upd
+            if epoch > burnin:
+                s = (epoch - burnin - 1) * nb + batch - 1
+                w_store[:, :, s] = w
+                U_store[:, :, :, :, s] = U
+            step += 1
+    return w_store, U_store, info
+
+
 RMS_LAMBDA = 1e-5   # GPT_SGLD.jl:1146 smoothing constant
 
 

@@ -196,6 +196,40 @@ def test_pred_mean_x_fused_features():
     assert np.abs(srm - want).max() <= 1e-12 * want.max()
 
 
+CLS_CASES = {
+    # name: (n, D, N, r, Q, m, C, burnin, maxepoch, langevin, stiefel)
+    "binary_sgld_stiefel": (16, 4, 60, 3, 20, 10, 2, 0, 2, True, True),
+    "three_class_ragged": (24, 3, 45, 2, 8, 16, 3, 1, 1, True, True),
+    "binary_sgd_stiefel": (16, 4, 60, 3, 20, 10, 2, 0, 1, False, True),
+    "binary_sgld_euclid": (16, 4, 60, 3, 20, 10, 2, 0, 1, True, False),
+    "binary_sgd_euclid": (16, 4, 60, 3, 20, 10, 2, 0, 1, False, False),
+}
+
+
+@pytest.mark.parametrize("name", list(CLS_CASES))
+def test_classification_matches_oracle(name):
+    """GPTclassification (GPT_SGLD.jl:452-680): softmax residuals over the classes, two moves
+    per step, all four langevin/stiefel variants of the second move."""
+    n, D, N, r, Q, m, ncls, burnin, maxepoch, lang, stf = CLS_CASES[name]
+    p = make_problem(n, D, N, r, Q, seed=23)
+    f = p["y"] - np.median(p["y"])
+    y = (1 + np.clip(np.floor((f - f.min()) / (np.ptp(f) + 1e-12) * ncls), 0, ncls - 1)).astype(float)
+    assert int(y.max()) == ncls and int(y.min()) == 1
+    epsw, epsU, seed = 1e-4, 1e-6, 41
+    ws, Us, dg = G().GPTclassification(p["phi"], y, p["I"], r, Q, m, epsw, epsU, burnin, maxepoch,
+                                       seed, langevin=lang, stiefel=stf, diag=True)
+    wo, Uo, info = R.GPTclassification(p["phi"], y, p["I"], r, Q, m, epsw, epsU, burnin, maxepoch,
+                                       seed, langevin=lang, stiefel=stf, record=True)
+    assert info["status"] == 0
+    assert ws.shape == (Q, ncls, maxepoch * (-(-N // m)))
+    assert rel(ws, wo) < 1e-8, rel(ws, wo)
+    assert rel(Us, Uo) < 1e-8, rel(Us, Uo)
+    gw = np.array(info["gradw_norm"])                  # (steps, C)
+    gu = np.array(info["gradU_norm"])                  # (steps, C, D)
+    assert rel(dg[0], gw) < 1e-9
+    assert rel(np.moveaxis(dg[1:], 0, 2), gu) < 1e-9
+
+
 WONLY_CASES = {
     # name: (n, D, N, r, Q, m, burnin, maxepoch, epsw)
     "small": (16, 3, 40, 2, 6, 8, 1, 2, 1e-4),

@@ -244,3 +244,32 @@ def test_sgldermw_oracle_keeps_U_and_matches_first_step():
     w1 = w0 + 1e-3 * g / 2 + math.sqrt(1e-3) * px.normals(Q, 5, 0, px.W_NOISE, 0)
     assert np.allclose(ws[:, 0], w1, rtol=0, atol=1e-13)
     assert abs(info["gradw_norm"][0] - np.linalg.norm(g)) < 1e-10 * np.linalg.norm(g)
+
+
+def test_classification_oracle_first_step_and_softmax_gradient():
+    """GPTclassification restatement: class-0 init equals GPTregression's (Stiefel), the
+    residual is [y = c] − softmax, and the gradient matches finite differences of the
+    multinomial log-likelihood Σ_i fhat[i, y_i] − logsumexp_i (the reference's check, :568-602)."""
+    rng = np.random.default_rng(12)
+    n, D, N, r, Q = 6, 2, 12, 2, 3
+    phi = rng.standard_normal((n, D, N))
+    I = R.samplenz(r, D, Q, 4)
+    w, U = R.init_state_cls(n, r, D, Q, 3, 9)
+    w0, U0 = R.init_state(n, r, D, Q, 9)
+    assert np.array_equal(w[:, 0], w0) and np.array_equal(U[..., 0], U0)
+    y = np.array([1, 2, 3] * 4)
+
+    def ll(wc):
+        f = np.stack([R.computefhat(R.computeV(R.phidotU(U[..., c], phi), I), wc[:, c])
+                      for c in range(3)], axis=1)
+        return sum(f[i, y[i] - 1] - R.logsumexp(f[i]) for i in range(N))
+    f = np.stack([R.computefhat(R.computeV(R.phidotU(U[..., c], phi), I), w[:, c]) for c in range(3)], axis=1)
+    lse = np.array([R.logsumexp(f[i]) for i in range(N)])
+    c = 1
+    res = (y == c + 1) - np.exp(f[:, c] - lse)
+    gw, gU = R.gradients_res(phi, res, w[:, c], U[..., c], I, N)
+    q, h = 2, 1e-6
+    wp = w.copy(); wp[q, c] += h
+    wm = w.copy(); wm[q, c] -= h
+    fd = (ll(wp) - ll(wm)) / (2 * h)
+    assert abs((gw[q] + w[q, c]) - fd) < 1e-6 * max(1.0, abs(fd))   # N/B = 1 here
