@@ -15,6 +15,8 @@ Same function names, argument meaning, return values and error behaviour as the 
     GPT_SGLDERMw(phi, y, signal_var, I, r, Q, m, epsw, burnin, maxepoch)  GPT_SGLD.jl:1065
     GPTclassification(phi, y, I, r, Q, m, epsw, epsU, burnin, maxepoch[, param_seed];
                       langevin, stiefel)                      GPT_SGLD.jl:452
+    GPT_GMC(phi, y, signal_var, I, r, Q, epsw, epsU, burnin, maxepoch, L, param_seed)
+                                                              GPT_SGLD.jl:684
     pred(w, U, I, phitest)                                    GPT_SGLD.jl:233
     RMSE(w_store, U_store, I, phitest, ytest)                 GPT_SGLD_p.jl:124
     pred_mean_x(w_store, U_store, I, Xtest, ytest, ls, σ, scale, Z, b)  fused feature + pred
@@ -307,6 +309,36 @@ def GPTclassification(phi, y, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_se
     else:
         check(code)
     return (w_store, U_store, dg) if diag else (w_store, U_store)
+
+
+def GPT_GMC(phi, y, signal_var, I, r, Q, epsw, epsU, burnin, maxepoch, L, param_seed=0,
+            w_init=None, U_init=None):
+    """Geodesic Monte Carlo (GPT_SGLD.jl:684-805).  Returns (w_store (Q, maxepoch),
+    U_store (n, r, D, maxepoch), accept_prob (burnin+maxepoch)); on the geodesic NaN bail-out
+    prints the reference's message and returns zeros and NaN probabilities."""
+    phi = _f64(phi)
+    n, D, N = phi.shape
+    y = _f64(np.asarray(y, dtype=np.float64).ravel())
+    if y.size != N:
+        raise ValueError("phi and y disagree on N")
+    I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+    if I.shape != (Q, D):
+        raise ValueError("I must be (Q, D)")
+    w_store = np.zeros((Q, maxepoch), order="F")
+    U_store = np.zeros((n, r, D, maxepoch), order="F")
+    acc = np.zeros(burnin + maxepoch)
+    wi = _f64(w_init) if w_init is not None else None
+    Ui = _f64(U_init) if U_init is not None else None
+    code = lib().gpt_gmc(_ptr(phi), _ptr(y), n, D, N, r, Q, _ptr(I, P_I32), float(signal_var),
+                         float(epsw), float(epsU), int(burnin), int(maxepoch), int(L),
+                         int(param_seed) & (2 ** 64 - 1), _ptr(wi) if wi is not None else None,
+                         _ptr(Ui) if Ui is not None else None, _ptr(w_store), _ptr(U_store),
+                         _ptr(acc))
+    if code == _lib.GPT_ERR_NAN_GEODESIC:
+        print("Get NaN when moving along Geodesic. Try smaller epsU")
+    else:
+        check(code)
+    return w_store, U_store, acc
 
 
 def GPT_SGLDERM(phi, y, sigma, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_seed=0, **kw):

@@ -78,6 +78,9 @@ SIGNATURES = {
                                   C.c_int64, C.c_double, P_D, P_D, P_D]),
     "gpt_sgld_classification": (C.c_int, [C.POINTER(SGLDConfig), P_D, P_D, P_I32, P_D, P_D, P_D,
                                           P_D, P_D]),
+    "gpt_gmc": (C.c_int, [P_D, P_D, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, P_I32,
+                          C.c_double, C.c_double, C.c_double, C.c_int64, C.c_int64, C.c_int64,
+                          C.c_uint64, P_D, P_D, P_D, P_D, P_D]),
     "gpt_tgp_gibbs": (C.c_int, [P_D, P_D, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                 C.c_double, C.c_int64, C.c_int64, C.c_uint64, P_I32, P_D, P_D,
                                 P_I32]),

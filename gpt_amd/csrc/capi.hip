@@ -1118,3 +1118,58 @@ extern "C" int gpt_tgp_gibbs(const double* b, const double* y, int64_t n, int64_
   HIPCHK(hipMemcpy(U_out, dUh.p, 8 * (size_t)nr * D * T, hipMemcpyDeviceToHost));
   return GPT_OK;
 }
+
+extern "C" int gpt_gmc(const double* phi, const double* y, int64_t n, int64_t D, int64_t N,
+                       int64_t r, int64_t Q, const int32_t* I, double signal_var, double epsw,
+                       double epsU, int64_t burnin, int64_t maxepoch, int64_t L, uint64_t seed,
+                       const double* w_init, const double* U_init, double* w_store,
+                       double* U_store, double* accept_prob) {
+  if (!phi || !y || !I || !w_store || !U_store || !accept_prob || n < 1 || D < 1 || N < 1 ||
+      Q < 1 || burnin < 0 || maxepoch < 0 || L < 1 || !(signal_var > 0)) {
+    set_error("bad GPT_GMC arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  if (!rank_supported((int)r) || !gmc_supported((int)n, (int)r)) {
+    set_error("GPT_GMC: rank not instantiated or n*r too large for one workgroup's LDS");
+    return GPT_ERR_BAD_DIMS;
+  }
+  std::vector<int32_t> I0((size_t)Q * D);
+  for (size_t x = 0; x < I0.size(); ++x) {
+    if (I[x] < 1 || I[x] > r) { set_error("I entries must be in 1..r"); return GPT_ERR_BAD_DIMS; }
+    I0[x] = I[x] - 1;
+  }
+  const size_t nm = (size_t)n * r * D, nphi = (size_t)n * D * N;
+  std::vector<double> w0((size_t)Q), U0(nm);
+  host_init_state((int)n, (int)r, (int)D, (int)Q, seed, true, 1.0, w0.data(), U0.data());
+  if (w_init) std::memcpy(w0.data(), w_init, 8 * (size_t)Q);
+  if (U_init) std::memcpy(U0.data(), U_init, 8 * nm);
+  DevMem dphi, dy, dI, dw, dU, dst;
+  HIPCHK(dphi.alloc(8 * nphi));
+  HIPCHK(dy.alloc(8 * (size_t)N));
+  HIPCHK(dI.alloc(4 * I0.size()));
+  HIPCHK(dw.alloc(8 * (size_t)Q));
+  HIPCHK(dU.alloc(8 * nm));
+  HIPCHK(dst.alloc(4));
+  HIPCHK(hipMemcpy(dphi.p, phi, 8 * nphi, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dy.p, y, 8 * (size_t)N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dI.p, I0.data(), 4 * I0.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dw.p, w0.data(), 8 * (size_t)Q, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dU.p, U0.data(), 8 * nm, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(dst.p, 0, 4));
+  std::memset(w_store, 0, 8 * (size_t)Q * maxepoch);
+  std::memset(U_store, 0, 8 * nm * maxepoch);
+  hipError_t e = gmc_run(dphi.as<double>(), dy.as<double>(), dI.as<int32_t>(), (int)n, (int)D, N,
+                         (int)r, (int)Q, signal_var, epsw, epsU, (int)burnin, (int)maxepoch, (int)L,
+                         seed, dw.as<double>(), dU.as<double>(), w_store, U_store, accept_prob,
+                         dst.as<int32_t>(), nullptr);
+  if (e != hipSuccess) return hip_fail(e, "GPT_GMC");
+  int32_t bad = 0;
+  HIPCHK(hipMemcpy(&bad, dst.p, 4, hipMemcpyDeviceToHost));
+  if (bad) {                         // GPT_SGLD.jl:757: zeros and NaN acceptance probabilities
+    std::memset(w_store, 0, 8 * (size_t)Q * maxepoch);
+    std::memset(U_store, 0, 8 * nm * maxepoch);
+    for (int64_t z = 0; z < burnin + maxepoch; ++z) accept_prob[z] = std::nan("");
+    set_error("Get NaN when moving along Geodesic. Try smaller epsU");
+    return GPT_ERR_NAN_GEODESIC;
+  }
+  return GPT_OK;
+}

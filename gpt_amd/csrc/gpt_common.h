@@ -15,7 +15,8 @@ namespace gpt {
 enum Stream : uint32_t {
   kWInit = 1, kUInit = 2, kPerm = 3, kWNoise = 4, kUNoise = 5,
   kThetaInit = 6, kThetaNoise = 7, kSampleNZ = 8, kFeatZ = 9, kFeatB = 10,
-  kTgpUInit = 11, kTgpI = 12, kTgpWNoise = 13, kTgpUNoise = 14
+  kTgpUInit = 11, kTgpI = 12, kTgpWNoise = 13, kTgpUNoise = 14,
+  kGmcP = 15, kGmcMom = 16, kGmcU = 17
 };
 
 struct U4 { uint32_t x, y, z, w; };

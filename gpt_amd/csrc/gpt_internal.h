@@ -158,6 +158,12 @@ hipError_t launch_feature(const double* X, long long N, int D, const double* ls,
 hipError_t launch_feature_notensor(const double* X, long long N, int D, const double* ls,
                                    double c, const double* Z, const double* b, int n,
                                    double* phi, hipStream_t st);
+bool gmc_supported(int n, int r);
+hipError_t gmc_run(const double* phi, const double* y, const int32_t* I0, int n, int D,
+                   long long N, int r, int Q, double signal_var, double epsw, double epsU,
+                   int burnin, int maxepoch, int L, uint64_t seed, double* w, double* U,
+                   double* w_store, double* U_store, double* accept, int32_t* status,
+                   hipStream_t st);
 hipError_t tgp_gibbs(const double* b, const double* y, int n, int D, long long N, int r, int q,
                      double sigma, int iters, int burnin, uint64_t seed, const int32_t* I0,
                      double* U, double* W_hist, double* U_hist, int32_t* status, hipStream_t st);

@@ -7,6 +7,7 @@
 // q ≈ 100, nr <= ~1000 in the reference's use, `UnitTest.jl:15-28`).  The feature contractions
 // reuse the phidotU tile of the SGLD path.
 #include "device_util.h"
+#include <cstdio>
 
 namespace gpt {
 
@@ -292,6 +293,363 @@ hipError_t tgp_gibbs(const double* b, const double* y, int n, int D, long long N
   }
   for (double* p : {temp, V, Cm, Ck, M, x, z, W, tnew})
     if (p) (void)hipFreeAsync(p, st);
+  return e;
+}
+
+// ============================================================================ GPT_GMC
+// Geodesic Monte Carlo (GPT_SGLD.jl:684-805): full-batch gradients from the same kernels as the
+// Gibbs sweep (temp over all N rows, V, the leave-one-out run sums C), then per-dimension
+// workgroups for the Stiefel kicks (proj) and the geodesic drift (geodboth, :40-59).
+
+// fhat[i] = Σ_q V[q,i]·w[q] (q ascending); res[i] = y[i] − fhat[i]
+__global__ void gmc_fhat_kernel(const double* __restrict__ V, const double* __restrict__ w,
+                                const double* __restrict__ y, int Q, long long N,
+                                double* __restrict__ fhat, double* __restrict__ res) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double s = 0.0;
+  for (int q = 0; q < Q; ++q) s = fma(V[q + (size_t)Q * i], w[q], s);
+  fhat[i] = s;
+  res[i] = y[i] - s;
+}
+
+// gw[q] = Σ_i V[q,i]·res[i] / σ² − w[q]   (σ_w = 1, GPT_SGLD.jl:725)
+__global__ void gmc_gradw_kernel(const double* __restrict__ V, const double* __restrict__ res,
+                                 const double* __restrict__ w, int Q, long long N, double inv_s2,
+                                 double* __restrict__ gw) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  double s = 0.0;
+  for (long long i = 0; i < N; ++i) s = fma(V[q + (size_t)Q * i], res[i], s);
+  gw[q] = s * inv_s2 - w[q];
+}
+
+// gU[j + n·l] = Σ_i C[l,i]·res[i]·phi[j,k,i] / σ²   (Ψ_k·res, :733-736)
+__global__ void gmc_gradU_kernel(const double* __restrict__ Cm, const double* __restrict__ res,
+                                 const double* __restrict__ phi, int n, int D, int R, long long N,
+                                 int k, double inv_s2, double* __restrict__ gU) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * R) return;
+  const int l = e / n, j = e - l * n;
+  double s = 0.0;
+  for (long long i = 0; i < N; ++i)
+    s = fma(Cm[l + (size_t)R * i] * res[i], phi[j + (size_t)n * (k + (size_t)D * i)], s);
+  gU[e] = s * inv_s2;
+}
+
+__global__ void gmc_axpy_kernel(double* __restrict__ x, const double* __restrict__ z, double a,
+                                int cnt) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < cnt) x[e] += a * z[e];
+}
+
+// Kick of U's momentum (one workgroup per dimension k): mom_k = proj(U_k, X), X = mom_k + c·gU_k,
+// or X = ξ (GMC_MOM stream, u_noise layout) when init (the fresh momentum of :711-713).
+template <int R>
+__global__ __launch_bounds__(kNT) void gmc_kick_kernel(const double* __restrict__ U,
+                                                       double* __restrict__ mom,
+                                                       const double* __restrict__ gU, double c,
+                                                       int n, int init, uint64_t seed,
+                                                       uint32_t epoch) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* Ul = (double*)smem;                 // n × R column-major
+  double* Xl = Ul + (size_t)n * R;
+  double* Ml = Xl + (size_t)n * R;            // R × R: Ml[a·R + b] = Σ_j U[j,a]·X[j,b]
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const size_t off = (size_t)n * R * k;
+  constexpr int RE = R + (R & 1);
+  for (int e = tid; e < n * R; e += kNT) {
+    Ul[e] = U[off + e];
+    if (!init) Xl[e] = mom[off + e] + c * gU[off + e];
+  }
+  if (init) {
+    for (int c0 = tid; c0 < (n * RE) / 2; c0 += kNT) {
+      double z0, z1;
+      normal_pair(seed, (uint32_t)c0, epoch, kGmcMom, (uint32_t)k, z0, z1);
+      const int e0 = 2 * c0, j = e0 / RE, l = e0 - j * RE;   // element l + RE·j
+      if (l < R) Xl[j + (size_t)n * l] = z0;
+      if (l + 1 < R) Xl[j + (size_t)n * (l + 1)] = z1;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < R * R; e += kNT) {
+    const int a = e / R, b = e - a * R;
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) s = fma(Ul[j + (size_t)n * a], Xl[j + (size_t)n * b], s);
+    Ml[e] = s;
+  }
+  __syncthreads();
+  for (int j = tid; j < n; j += kNT) {
+#pragma unroll
+    for (int b = 0; b < R; ++b) {
+      double s = 0.0;
+#pragma unroll
+      for (int a = 0; a < R; ++a) s = fma(Ul[j + (size_t)n * a], Ml[a * R + b] + Ml[b * R + a], s);
+      mom[off + j + (size_t)n * b] = Xl[j + (size_t)n * b] - s / 2;
+    }
+  }
+}
+
+// Drift of U_k along its geodesic for time t (geodboth, :40-59), one workgroup per dimension:
+// E = expm(t[A −S; I A]) (wave 0), expm(−tA) (wave 1), U ← normalise([U mom]·E[:,1:r]·expm(−tA)),
+// mom ← [U mom]·E[:,r+1:2r]·expm(−tA).  status = 1 on a NaN in E.
+template <int R>
+__global__ __launch_bounds__(kNT) void gmc_geod_kernel(double* __restrict__ U,
+                                                       double* __restrict__ mom, double t, int n,
+                                                       int32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NN = 2 * R;
+  double* Ul = (double*)smem;
+  double* Ml = Ul + (size_t)n * R;
+  double* Ag = Ml + (size_t)n * R;           // R × R   Uᵀmom
+  double* Sg = Ag + R * R;                   // R × R   momᵀmom
+  double* X0 = Sg + R * R;                   // 7·NN² expm scratch (E at X0 + NN²)
+  double* X1 = X0 + 7 * NN * NN;             // 7·R² expm scratch (expm(−tA) at X1 + R²)
+  double* F = X1 + 7 * R * R;                // NN × NN: [E[:,1:r]·mx | E[:,r+1:2r]·mx]
+  double* nr = F + NN * NN;                  // R column norms
+  int& bad = *(int*)(nr + R);                // NaN flag of the expm
+  const int k = blockIdx.x, tid = threadIdx.x, wv = tid >> 6;
+  const size_t off = (size_t)n * R * k;
+  for (int e = tid; e < n * R; e += kNT) { Ul[e] = U[off + e]; Ml[e] = mom[off + e]; }
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  for (int e = tid; e < 2 * R * R; e += kNT) {
+    const int g = e / (R * R), ab = e - g * R * R, a = ab / R, b = ab - a * R;
+    const double* P = g ? Ml : Ul;
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) s = fma(P[j + (size_t)n * a], Ml[j + (size_t)n * b], s);
+    (g ? Sg : Ag)[ab] = s;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    for (int o = tid; o < NN * NN; o += 64) {
+      const int i = o / NN, j = o - i * NN;
+      double v;
+      if (i < R) v = j < R ? Ag[i * R + j] : -Sg[i * R + (j - R)];
+      else v = j < R ? (i - R == j ? 1.0 : 0.0) : Ag[(i - R) * R + (j - R)];
+      X0[o] = t * v;
+    }
+    wave_sync();
+    if (wave_expm<NN>(X0) && tid == 0) bad = 1;
+  } else if (wv == 1) {
+    const int ln = tid & 63;
+    for (int o = ln; o < R * R; o += 64) X1[o] = -t * Ag[o];
+    wave_sync();
+    wave_expm<R>(X1);
+  }
+  __syncthreads();
+  if (bad) {
+    if (tid == 0) *status = 1;
+    return;
+  }
+  const double* E = X0 + NN * NN;
+  const double* mx = X1 + R * R;
+  for (int o = tid; o < NN * NN; o += kNT) {       // F[a][h·R + l] = Σ_c E[a][h·R + c]·mx[c][l]
+    const int a = o / NN, hl = o - a * NN, h = hl / R, l = hl - h * R;
+    double s = 0.0;
+#pragma unroll
+    for (int c2 = 0; c2 < R; ++c2) s = fma(E[a * NN + h * R + c2], mx[c2 * R + l], s);
+    F[o] = s;
+  }
+  __syncthreads();
+  for (int j = tid; j < n; j += kNT) {
+    double x[NN];
+#pragma unroll
+    for (int a = 0; a < R; ++a) { x[a] = Ul[j + (size_t)n * a]; x[R + a] = Ml[j + (size_t)n * a]; }
+#pragma unroll
+    for (int hl = 0; hl < NN; ++hl) {
+      double s = 0.0;
+#pragma unroll
+      for (int a = 0; a < NN; ++a) s = fma(x[a], F[a * NN + hl], s);
+      if (hl < R) Ul[j + (size_t)n * hl] = s;                 // tmpU (normalised below)
+      else mom[off + j + (size_t)n * (hl - R)] = s;           // tmpV
+    }
+  }
+  __syncthreads();
+  for (int l = tid; l < R; l += kNT) {
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) s = fma(Ul[j + (size_t)n * l], Ul[j + (size_t)n * l], s);
+    nr[l] = sqrt(s);
+  }
+  __syncthreads();
+  for (int e = tid; e < n * R; e += kNT) U[off + e] = Ul[e] / nr[e / n];
+}
+
+// out[0] = −|w|²/2 − |res|²/(2σ²) − |mom|²/2 − |p|²/2   (H, GPT_SGLD.jl:714, :795)
+__global__ __launch_bounds__(kNT) void gmc_energy_kernel(const double* __restrict__ w,
+                                                         const double* __restrict__ p, int Q,
+                                                         const double* __restrict__ res,
+                                                         long long N, const double* __restrict__ mom,
+                                                         long long nm, double inv_2s2,
+                                                         double* __restrict__ out) {
+  __shared__ double red[kNW];
+  double a = 0.0, b = 0.0, c = 0.0, d = 0.0;
+  for (int q = threadIdx.x; q < Q; q += kNT) { a = fma(w[q], w[q], a); d = fma(p[q], p[q], d); }
+  for (long long i = threadIdx.x; i < N; i += kNT) b = fma(res[i], res[i], b);
+  for (long long e = threadIdx.x; e < nm; e += kNT) c = fma(mom[e], mom[e], c);
+  const double sa = blk_sum(a, red), sb = blk_sum(b, red), sc = blk_sum(c, red), sd = blk_sum(d, red);
+  if (threadIdx.x == 0) out[0] = -sa / 2 - sb * inv_2s2 - sc / 2 - sd / 2;
+}
+
+static size_t gmc_kick_lds(int n, int r) { return 8 * ((size_t)2 * n * r + (size_t)r * r); }
+static size_t gmc_geod_lds(int n, int r) {
+  return 8 * ((size_t)2 * n * r + 2 * (size_t)r * r + 7 * 4 * (size_t)r * r + 7 * (size_t)r * r +
+              4 * (size_t)r * r + r + 1);
+}
+
+bool gmc_supported(int n, int r) {
+  return gmc_geod_lds(n, r) <= 160 * 1024 && gmc_kick_lds(n, r) <= 160 * 1024;
+}
+
+static hipError_t launch_gmc_kick(const double* U, double* mom, const double* gU, double c, int n,
+                                  int D, int r, int init, uint64_t seed, uint32_t epoch,
+                                  hipStream_t st) {
+  const size_t lds = gmc_kick_lds(n, r);
+  switch (r) {
+#define CASE(RR)                                                                              \
+  case RR: {                                                                                  \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      hipError_t e = hipFuncSetAttribute((const void*)gmc_kick_kernel<RR>,                     \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      if (e != hipSuccess) return e;                                                          \
+      attr = true;                                                                            \
+    }                                                                                         \
+    hipLaunchKernelGGL(gmc_kick_kernel<RR>, dim3(D), dim3(kNT), lds, st, U, mom, gU, c, n, init, \
+                       seed, epoch);                                                          \
+  } break;
+    GPT_TGP_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+static hipError_t launch_gmc_geod(double* U, double* mom, double t, int n, int D, int r,
+                                  int32_t* status, hipStream_t st) {
+  const size_t lds = gmc_geod_lds(n, r);
+  switch (r) {
+#define CASE(RR)                                                                              \
+  case RR: {                                                                                  \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      hipError_t e = hipFuncSetAttribute((const void*)gmc_geod_kernel<RR>,                     \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      if (e != hipSuccess) return e;                                                          \
+      attr = true;                                                                            \
+    }                                                                                         \
+    hipLaunchKernelGGL(gmc_geod_kernel<RR>, dim3(D), dim3(kNT), lds, st, U, mom, t, n, status); \
+  } break;
+    GPT_TGP_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// Full-data gradients at (w, U): fhat/res, gw, gU (all device; scratch temp (D·r·N), V (Q·N),
+// Cm (r·N)).
+static hipError_t gmc_gradients(const double* phi, const double* y, const int32_t* I0,
+                                 const double* w, const double* U, int n, int D, long long N,
+                                 int r, int Q, double inv_s2, double* temp, double* V, double* Cm,
+                                 double* fhat, double* res, double* gw, double* gU,
+                                 hipStream_t st) {
+  hipError_t e = launch_tgp_temp(U, phi, n, D, N, r, 0, D, temp, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tgp_v_kernel, nblk((long long)Q * N, 256), 256, 0, st, temp, I0, Q, D, r, N, V);
+  hipLaunchKernelGGL(gmc_fhat_kernel, nblk(N, 256), 256, 0, st, V, w, y, Q, N, fhat, res);
+  hipLaunchKernelGGL(gmc_gradw_kernel, nblk(Q, 64), 64, 0, st, V, res, w, Q, N, inv_s2, gw);
+  for (int k = 0; k < D; ++k) {
+    hipLaunchKernelGGL(tgp_c_kernel, nblk((long long)r * N, 256), 256, 0, st, V, w, temp, I0, Q, r,
+                       N, k, Cm);
+    hipLaunchKernelGGL(gmc_gradU_kernel, nblk((long long)n * r, 64), 64, 0, st, Cm, res, phi, n, D,
+                       r, N, k, inv_s2, gU + (size_t)n * r * k);
+  }
+  return hipGetLastError();
+}
+
+hipError_t gmc_run(const double* phi, const double* y, const int32_t* I0, int n, int D,
+                   long long N, int r, int Q, double signal_var, double epsw, double epsU,
+                   int burnin, int maxepoch, int L, uint64_t seed, double* w, double* U,
+                   double* w_store, double* U_store, double* accept, int32_t* status,
+                   hipStream_t st) {
+  const size_t nm = (size_t)n * r * D;
+  const double inv_s2 = 1.0 / signal_var, sw = sqrt(epsw), su = sqrt(epsU);
+  double *temp = nullptr, *V = nullptr, *Cm = nullptr, *fhat = nullptr, *res = nullptr,
+         *gw = nullptr, *gU = nullptr, *p = nullptr, *mom = nullptr, *w_old = nullptr, *Hd = nullptr;
+  hipError_t e = hipSuccess;
+  auto al = [&](double** q, size_t cnt) {
+    if (e == hipSuccess) e = hipMallocAsync((void**)q, 8 * (cnt ? cnt : 1), st);
+  };
+  al(&temp, (size_t)D * r * N); al(&V, (size_t)Q * N); al(&Cm, (size_t)r * N); al(&fhat, N);
+  al(&res, N); al(&gw, Q); al(&gU, nm); al(&p, Q); al(&mom, nm); al(&w_old, Q); al(&Hd, 2);
+#define GMC_CK(stage)                                                                        \
+  do {                                                                                       \
+    if (e == hipSuccess) e = hipGetLastError();                                              \
+    if (e != hipSuccess) {                                                                   \
+      fprintf(stderr, "gpt_gmc: %s failed: %s\n", stage, hipGetErrorString(e));              \
+    }                                                                                        \
+  } while (0)
+  GMC_CK("alloc");
+  auto grads = [&]() {
+    return gmc_gradients(phi, y, I0, w, U, n, D, N, r, Q, inv_s2, temp, V, Cm, fhat, res, gw, gU, st);
+  };
+  auto kick = [&]() {
+    hipLaunchKernelGGL(gmc_axpy_kernel, nblk(Q, 256), 256, 0, st, p, gw, sw / 2, Q);
+    return launch_gmc_kick(U, mom, gU, su / 2, n, D, r, 0, seed, 0, st);
+  };
+  for (int epoch = 1; epoch <= burnin + maxepoch && e == hipSuccess; ++epoch) {
+    e = hipMemcpyAsync(w_old, w, 8 * (size_t)Q, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) break;
+    hipLaunchKernelGGL(normals_kernel, nblk(Q, 256), 256, 0, st, p, Q, seed, (uint32_t)(epoch - 1),
+                       (uint32_t)kGmcP, 0u);
+    e = launch_gmc_kick(U, mom, nullptr, 0.0, n, D, r, 1, seed, (uint32_t)(epoch - 1), st);
+    GMC_CK("momentum draw");
+    if (e == hipSuccess) e = grads();
+    GMC_CK("gradients");
+    if (e != hipSuccess) break;
+    hipLaunchKernelGGL(gmc_energy_kernel, 1, kNT, 0, st, w, p, Q, res, N, mom, (long long)nm,
+                       inv_s2 / 2, Hd);
+    for (int l = 0; l < L && e == hipSuccess; ++l) {
+      e = kick();
+      if (e != hipSuccess) break;
+      hipLaunchKernelGGL(gmc_axpy_kernel, nblk(Q, 256), 256, 0, st, w, p, sw, Q);
+      GMC_CK("kick/drift");
+      if (e == hipSuccess) e = launch_gmc_geod(U, mom, su, n, D, r, status, st);
+      GMC_CK("geodesic");
+      if (e == hipSuccess) e = grads();
+      GMC_CK("gradients");
+      if (e == hipSuccess) e = kick();
+      GMC_CK("kick");
+    }
+    if (e != hipSuccess) break;
+    hipLaunchKernelGGL(gmc_energy_kernel, 1, kNT, 0, st, w, p, Q, res, N, mom, (long long)nm,
+                       inv_s2 / 2, Hd + 1);
+    double H[2];
+    int32_t bad = 0;
+    e = hipMemcpyAsync(H, Hd, 16, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, status, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    GMC_CK("energy");
+    if (e != hipSuccess || bad) break;
+    const double ap = exp(H[1] - H[0]);
+    accept[epoch - 1] = ap;
+    const U4 x = philox4x32(0u, (uint32_t)(epoch - 1), kGmcU, 0u, seed);
+    if (u53(x.x, x.y) > ap)                  // reject: w only (U_old aliases U, :710/:798-800)
+      e = hipMemcpyAsync(w, w_old, 8 * (size_t)Q, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && epoch > burnin) {
+      e = hipMemcpyAsync(w_store + (size_t)Q * (epoch - burnin - 1), w, 8 * (size_t)Q,
+                         hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(U_store + nm * (epoch - burnin - 1), U, 8 * nm, hipMemcpyDeviceToHost, st);
+    }
+  }
+  GMC_CK("stores");
+#undef GMC_CK
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  for (double* q : {temp, V, Cm, fhat, res, gw, gU, p, mom, w_old, Hd})
+    if (q) (void)hipFreeAsync(q, st);
+  (void)hipStreamSynchronize(st);
   return e;
 }
 

@@ -194,6 +194,17 @@ int gpt_tgp_gibbs(const double* b, const double* y, int64_t n, int64_t D, int64_
                   int64_t q, double sigma, int64_t num_iterations, int64_t burnin, uint64_t seed,
                   const int32_t* I, double* W_out, double* U_out, int32_t* I_out);
 
+/* ---- geodesic Monte Carlo (§8(f) item 4) ------------------------------------------- */
+/* GPT_GMC(phi,y,signal_var,I,r,Q,epsw,epsU,burnin,maxepoch,L,param_seed)  GPT_SGLD.jl:684-805:
+ * full-batch HMC with L leapfrog steps per epoch (Stiefel geodesic drift for U, geodboth
+ * :40-59), sigma_w = 1.  w_store (Q, maxepoch), U_store (n, r, D, maxepoch), accept_prob
+ * (burnin+maxepoch).  As the reference, a rejection restores w only (U_old aliases U there).
+ * Optional w_init (Q) / U_init (n, r, D).  GPT_ERR_NAN_GEODESIC: zero stores, NaN accept_prob. */
+int gpt_gmc(const double* phi, const double* y, int64_t n, int64_t D, int64_t N, int64_t r,
+            int64_t Q, const int32_t* I, double signal_var, double epsw, double epsU,
+            int64_t burnin, int64_t maxepoch, int64_t L, uint64_t seed, const double* w_init,
+            const double* U_init, double* w_store, double* U_store, double* accept_prob);
+
 const char* gpt_last_error(void);
 /* LDS bytes one step workgroup needs for this shape (must be <= 163840). */
 int64_t gpt_sgld_lds_bytes(int64_t n, int64_t D, int64_t r, int64_t Q, int64_t m);

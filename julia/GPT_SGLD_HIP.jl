@@ -9,7 +9,7 @@
 module GPT_SGLD_HIP
 
 export datawhitening, feature, featureNotensor, samplenz, GPTregression, GPT_SGLDERM, pred, RMSE,
-       GPNT_SGLD, GPT_SGLDERM_RMSprop, GPT_SGLDERMw, GPTclassification
+       GPNT_SGLD, GPT_SGLDERM_RMSprop, GPT_SGLDERMw, GPTclassification, GPT_GMC
 
 const LIB = get(ENV, "GPTSGLD_LIB", joinpath(@__DIR__, "..", "gpt_amd", "libgptsgld.so"))
 
@@ -164,6 +164,24 @@ function GPTclassification(phi::Array{Float64,3}, y::Array, I::Array{Int32,2}, r
     end
     check(rc)
     return w_store, U_store
+end
+
+# GPT_SGLD.jl:684-805 (geodesic Monte Carlo)
+function GPT_GMC(phi::Array{Float64,3}, y::Array{Float64}, signal_var::Real, I::Array{Int32,2},
+                 r::Integer, Q::Integer, epsw::Real, epsU::Real, burnin::Integer, maxepoch::Integer,
+                 L::Integer, param_seed::Integer)
+    n, D, N = size(phi)
+    w_store = Array{Float64}(undef, Q, maxepoch); U_store = Array{Float64}(undef, n, r, D, maxepoch)
+    accept_prob = Array{Float64}(undef, maxepoch + burnin)
+    rc = ccall((:gpt_gmc, LIB), Cint,
+               (Ptr{Float64}, Ptr{Float64}, Int64, Int64, Int64, Int64, Int64, Ptr{Int32}, Float64,
+                Float64, Float64, Int64, Int64, Int64, UInt64, Ptr{Float64}, Ptr{Float64},
+                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+               phi, vec(y), n, D, N, r, Q, I, signal_var, epsw, epsU, burnin, maxepoch, L, param_seed,
+               C_NULL, C_NULL, w_store, U_store, accept_prob)
+    rc == 1 && println("Get NaN when moving along Geodesic. Try smaller epsU")
+    rc in (0, 1) || check(rc)
+    return w_store, U_store, accept_prob
 end
 
 function pred(w::Array{Float64}, U::Array{Float64,3}, I::Array{Int32,2}, phitest::Array{Float64,3})

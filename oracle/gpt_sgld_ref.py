@@ -532,6 +532,97 @@ def GPTclassification(phi, y, I, r, Q, m, epsw, epsU, burnin, maxepoch, param_se
     return w_store, U_store, info
 
 
+def geodboth(U, mom, t):
+    """GPT_SGLD.jl:40-59: geodesic end point AND its velocity; (zeros, zeros, False) on NaN."""
+    n, r = U.shape
+    A = U.T @ mom
+    T = np.block([[A, -(mom.T @ mom)], [np.eye(r), A]])
+    with np.errstate(all="ignore"):
+        E = expm(t * T)
+    if np.isnan(E).any():
+        return np.zeros((n, r)), np.zeros((n, r)), False
+    mexp = expm(-t * A)
+    X = np.hstack([U, mom])
+    tmpU = (X @ E[:, :r]) @ mexp
+    tmpV = (X @ E[:, r:]) @ mexp
+    return tmpU / np.linalg.norm(tmpU, axis=0)[None, :], tmpV, True
+
+
+def full_gradients(phi, y, w, U, I, signal_var):
+    """GPT_GMC's full-data gradients (GPT_SGLD.jl:718-739): gradw = V(y−fhat)/σ² − w (σ_w = 1),
+    gradU_k = Ψ_k(y−fhat)/σ²; also fhat."""
+    n, D, N = phi.shape
+    r = U.shape[1]
+    temp = phidotU(U, phi)
+    V = computeV(temp, I)
+    fhat = computefhat(V, w)
+    res = y - fhat
+    gradw = V @ res / signal_var - w
+    Psi = computePsi(computeA(computeU_phi(V, temp, I), w, I, r), phi)
+    gradU = np.empty((n, r, D))
+    for k in range(D):
+        gradU[:, :, k] = (Psi[:, :, k] @ res / signal_var).reshape((n, r), order="F")
+    return gradw, gradU, fhat
+
+
+def GPT_GMC(phi, y, signal_var, I, r, Q, epsw, epsU, burnin, maxepoch, L, param_seed,
+            w_init=None, U_init=None):
+    """GPT_SGLD.jl:684-805 — geodesic Monte Carlo (full-batch HMC with the Stiefel geodesic
+    flow for U), σ_w = 1.  Per epoch: p ~ N(0, I) (GMC_P stream), mom_k = proj(U_k, ξ) (GMC_MOM,
+    u_noise layout), L leapfrog steps (half kick, drift: w += √εw·p and geodboth, half kick),
+    H = −|w|²/2 − |y−fhat|²/(2σ²) − |mom|²/2 − |p|²/2, accept_prob = exp(H − H_old), reject
+    when u > accept_prob (u on GMC_U).  As in the reference, a rejection restores w only:
+    ``U_old = U`` aliases the array that the leapfrog updates in place (:710, :754), so U keeps
+    its proposal.  Returns (w_store (Q, maxepoch), U_store (n, r, D, maxepoch), accept_prob);
+    a NaN in a geodesic returns zeros and NaN accept probabilities (:757)."""
+    phi = np.asarray(phi, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64).ravel()
+    n, D, N = phi.shape
+    if w_init is None or U_init is None:
+        w0, U0 = init_state(n, r, D, Q, param_seed, True, 1.0)
+    w = np.array(w0 if w_init is None else w_init, dtype=np.float64)
+    U = np.array(U0 if U_init is None else U_init, dtype=np.float64, order="F")
+    w_store = np.zeros((Q, maxepoch), order="F")
+    U_store = np.zeros((n, r, D, maxepoch), order="F")
+    acc = np.zeros(maxepoch + burnin)
+    sw, su = math.sqrt(epsw), math.sqrt(epsU)
+    re = r + (r & 1)
+    for epoch in range(1, burnin + maxepoch + 1):
+        w_old = w
+        p = px.normals(Q, param_seed, epoch - 1, px.GMC_P, 0)
+        mom = np.empty((n, r, D), order="F")
+        for k in range(D):
+            xi = px.normals(re * n, param_seed, epoch - 1, px.GMC_MOM, k).reshape((n, re))[:, :r]
+            mom[:, :, k] = proj(U[:, :, k], xi)
+        H_old = (-np.sum(w * w) / 2 - np.linalg.norm(y - pred(w, U, I, phi)) ** 2 / (2 * signal_var)
+                 - np.sum(mom * mom) / 2 - np.sum(p * p) / 2)
+        gw, gU, fhat = full_gradients(phi, y, w, U, I, signal_var)
+        for _ in range(L):
+            p = p + sw * gw / 2
+            for k in range(D):
+                mom[:, :, k] = proj(U[:, :, k], mom[:, :, k] + su * gU[:, :, k] / 2)
+            w = w + sw * p
+            for k in range(D):
+                Un, Vn, ok = geodboth(U[:, :, k], mom[:, :, k], su)
+                if not ok:
+                    return (np.zeros((Q, maxepoch)), np.zeros((n, r, D, maxepoch)),
+                            np.full(maxepoch + burnin, np.nan))
+                U[:, :, k], mom[:, :, k] = Un, Vn
+            gw, gU, fhat = full_gradients(phi, y, w, U, I, signal_var)   # also the next kick's
+            p = p + sw * gw / 2
+            for k in range(D):
+                mom[:, :, k] = proj(U[:, :, k], mom[:, :, k] + su * gU[:, :, k] / 2)
+        H = (-np.sum(w * w) / 2 - np.linalg.norm(y - fhat) ** 2 / (2 * signal_var)
+             - np.sum(mom * mom) / 2 - np.sum(p * p) / 2)
+        acc[epoch - 1] = math.exp(H - H_old)
+        if px.uniform(param_seed, epoch - 1, px.GMC_U, 0) > acc[epoch - 1]:
+            w = w_old                                       # U stays (reference aliasing)
+        if epoch > burnin:
+            w_store[:, epoch - burnin - 1] = w
+            U_store[:, :, :, epoch - burnin - 1] = U
+    return w_store, U_store, acc
+
+
 RMS_LAMBDA = 1e-5   # GPT_SGLD.jl:1146 smoothing constant
 
 

@@ -38,6 +38,8 @@ MASK32 = np.uint64(0xFFFFFFFF)
 W_INIT, U_INIT, PERM, W_NOISE, U_NOISE, THETA_INIT, THETA_NOISE = 1, 2, 3, 4, 5, 6, 7
 # TGP Gibbs (TGP.jl:37-86): U init, the core index draw, and the two Gaussian draws per sweep
 TGP_U_INIT, TGP_I, TGP_W_NOISE, TGP_U_NOISE = 11, 12, 13, 14
+# GPT_GMC (GPT_SGLD.jl:684-805): momentum of w, momentum of U, the accept/reject uniform
+GMC_P, GMC_MOM, GMC_U = 15, 16, 17
 
 
 def philox4x32(c0, c1, c2, c3, seed):
@@ -85,6 +87,12 @@ def normals(count, seed, c1, c2, c3):
     z[0::2] = rad * np.cos(th)
     z[1::2] = rad * np.sin(th)
     return z[:count]
+
+
+def uniform(seed, c1, c2, c3):
+    """One uniform on (0, 1): u53 of the first two words of Philox block 0 of (c1, c2, c3)."""
+    x0, x1, _, _ = philox4x32(np.zeros(1, dtype=np.uint32), c1, c2, c3, seed)
+    return float(_u53(x0, x1)[0])
 
 
 def randperm(N, seed, epoch):

@@ -230,6 +230,43 @@ def test_classification_matches_oracle(name):
     assert rel(np.moveaxis(dg[1:], 0, 2), gu) < 1e-9
 
 
+GMC_CASES = {
+    # name: (n, D, N, r, Q, L, burnin, maxepoch, signal_var, eps)
+    "accepting": (8, 3, 40, 2, 5, 5, 1, 5, 1.0, 1e-2),
+    "rejecting": (8, 3, 40, 2, 5, 5, 1, 7, 1.0, 1e-1),   # epochs 1, 4, 6, 7 rejected (w restored)
+    "powerplant_like": (20, 4, 300, 5, 40, 4, 0, 2, 1.0, 1e-3),
+}
+
+
+def _gmc_problem(n, D, N, r, Q):
+    rng = np.random.default_rng(3)
+    phi = rng.standard_normal((n, D, N)) * 0.5
+    I = R.samplenz(r, D, Q, 1)
+    w, U = R.init_state(n, r, D, Q, 3)
+    return phi, R.pred(w, U, I, phi) + 0.1 * rng.standard_normal(N), I
+
+
+@pytest.mark.parametrize("name", list(GMC_CASES))
+def test_gmc_matches_oracle(name):
+    """GPT_GMC (GPT_SGLD.jl:684-805): full-batch leapfrog with geodboth, Metropolis step."""
+    n, D, N, r, Q, L, burnin, maxepoch, sv, eps = GMC_CASES[name]
+    phi, y, I = _gmc_problem(n, D, N, r, Q)
+    ws, Us, acc = G().GPT_GMC(phi, y, sv, I, r, Q, eps, eps, burnin, maxepoch, L, 7)
+    wo, Uo, acco = R.GPT_GMC(phi, y, sv, I, r, Q, eps, eps, burnin, maxepoch, L, 7)
+    assert rel(ws, wo) < 1e-8, rel(ws, wo)
+    assert rel(Us, Uo) < 1e-8, rel(Us, Uo)
+    assert np.all(np.abs(acc - acco) <= 1e-7 * np.maximum(np.abs(acco), 1e-3))
+
+
+def test_gmc_geodesic_nan_bailout():
+    """A diverging geodesic returns zero stores and NaN acceptance probabilities (:757)."""
+    phi, y, I = _gmc_problem(8, 3, 40, 2, 5)
+    ws, Us, acc = G().GPT_GMC(phi, y, 0.1, I, 2, 5, 0.3, 0.3, 1, 3, 5, 7)
+    wo, Uo, acco = R.GPT_GMC(phi, y, 0.1, I, 2, 5, 0.3, 0.3, 1, 3, 5, 7)
+    assert np.isnan(acco).all() and np.isnan(acc).all()
+    assert not ws.any() and not Us.any()
+
+
 WONLY_CASES = {
     # name: (n, D, N, r, Q, m, burnin, maxepoch, epsw)
     "small": (16, 3, 40, 2, 6, 8, 1, 2, 1e-4),

@@ -273,3 +273,22 @@ def test_classification_oracle_first_step_and_softmax_gradient():
     wm = w.copy(); wm[q, c] -= h
     fd = (ll(wp) - ll(wm)) / (2 * h)
     assert abs((gw[q] + w[q, c]) - fd) < 1e-6 * max(1.0, abs(fd))   # N/B = 1 here
+
+
+def test_gmc_oracle_energy_conservation_and_w_only_rejection():
+    """GPT_GMC restatement: the leapfrog conserves H to O(ε) (acceptance → 1 as ε → 0), and a
+    rejected epoch restores w but keeps U's proposal (the reference's U_old aliasing)."""
+    rng = np.random.default_rng(3)
+    n, D, N, r, Q = 8, 3, 40, 2, 5
+    phi = rng.standard_normal((n, D, N)) * 0.5
+    I = R.samplenz(r, D, Q, 1)
+    w, U = R.init_state(n, r, D, Q, 3)
+    y = R.pred(w, U, I, phi) + 0.1 * rng.standard_normal(N)
+    _, _, acc = R.GPT_GMC(phi, y, 1.0, I, r, Q, 1e-7, 1e-7, 0, 2, 3, 7)
+    assert np.all(np.abs(acc - 1) < 1e-3)
+    ws, Us, acc = R.GPT_GMC(phi, y, 1.0, I, r, Q, 0.1, 0.1, 0, 1, 5, 7)
+    u = px.uniform(7, 0, px.GMC_U, 0)
+    w0, U0 = R.init_state(n, r, D, Q, 7)
+    assert u > acc[0]                                   # this epoch is rejected
+    assert np.array_equal(ws[:, 0], w0)                 # w restored
+    assert not np.allclose(Us[..., 0], U0)              # U keeps the proposal
