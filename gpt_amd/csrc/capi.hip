@@ -84,12 +84,38 @@ static void jacobi_eig(int r, std::vector<double>& A, std::vector<double>& V,
 }
 
 // GPT_SGLD.jl:357-369: w = σ_w·randn(Q); U_k = Zᵀ(ZZᵀ)^(-1/2), Z = randn(r,n)  (or randn/√n).
+// Uniform draw on the Stiefel manifold from Z (r × n, element a + r·j): Uk (n × r, column-major)
+// = Zᵀ(ZZᵀ)^(-1/2), the polar factor (transpose(sqrtm(Z*Z') \\ Z), GPT_SGLD.jl:365-366).
+static void host_stiefel_polar(const double* Z, int r, int n, double* Uk) {
+  std::vector<double> G((size_t)r * r, 0.0), Vv, ev;
+  for (int a = 0; a < r; ++a)
+    for (int c = 0; c < r; ++c) {
+      double s = 0.0;
+      for (int j = 0; j < n; ++j) s += Z[a + (size_t)r * j] * Z[c + (size_t)r * j];
+      G[a * r + c] = s;
+    }
+  jacobi_eig(r, G, Vv, ev);
+  std::vector<double> S((size_t)r * r, 0.0);  // (ZZᵀ)^(-1/2)
+  for (int a = 0; a < r; ++a)
+    for (int c = 0; c < r; ++c) {
+      double s = 0.0;
+      for (int z = 0; z < r; ++z) s += Vv[a * r + z] * Vv[c * r + z] / std::sqrt(ev[z]);
+      S[a * r + c] = s;
+    }
+  for (int j = 0; j < n; ++j)
+    for (int c = 0; c < r; ++c) {
+      double s = 0.0;
+      for (int a = 0; a < r; ++a) s += Z[a + (size_t)r * j] * S[a * r + c];
+      Uk[j + (size_t)n * c] = s;
+    }
+}
+
 // Class cls of GPTclassification (GPT_SGLD.jl:463-477) draws w on (W_INIT, cls) and U_k on
 // (U_INIT, k + D·cls), and its non-Stiefel U is randn unscaled (cls_init).
 void host_init_state(int n, int r, int D, int Q, uint64_t seed, bool stiefel, double sigma_w,
                      double* w, double* U, int cls, bool cls_init) {
   for (int q = 0; q < Q; ++q) w[q] = sigma_w * host_normal(seed, q, 0, kWInit, (uint32_t)cls);
-  std::vector<double> Z((size_t)r * n), G, Vv, ev;
+  std::vector<double> Z((size_t)r * n);
   for (int k = 0; k < D; ++k) {
     for (int e = 0; e < r * n; ++e) Z[e] = host_normal(seed, e, 0, kUInit, (uint32_t)(k + D * cls));  // Z[a + r*j]
     double* Uk = U + (size_t)n * r * k;
@@ -98,27 +124,7 @@ void host_init_state(int n, int r, int D, int Q, uint64_t seed, bool stiefel, do
         for (int a = 0; a < r; ++a) Uk[j + (size_t)n * a] = cls_init ? Z[a + (size_t)r * j] : Z[a + (size_t)r * j] / std::sqrt((double)n);
       continue;
     }
-    G.assign((size_t)r * r, 0.0);
-    for (int a = 0; a < r; ++a)
-      for (int c = 0; c < r; ++c) {
-        double s = 0.0;
-        for (int j = 0; j < n; ++j) s += Z[a + (size_t)r * j] * Z[c + (size_t)r * j];
-        G[a * r + c] = s;
-      }
-    jacobi_eig(r, G, Vv, ev);
-    std::vector<double> S((size_t)r * r, 0.0);  // (ZZᵀ)^(-1/2)
-    for (int a = 0; a < r; ++a)
-      for (int c = 0; c < r; ++c) {
-        double s = 0.0;
-        for (int z = 0; z < r; ++z) s += Vv[a * r + z] * Vv[c * r + z] / std::sqrt(ev[z]);
-        S[a * r + c] = s;
-      }
-    for (int j = 0; j < n; ++j)
-      for (int c = 0; c < r; ++c) {
-        double s = 0.0;
-        for (int a = 0; a < r; ++a) s += Z[a + (size_t)r * j] * S[a * r + c];
-        Uk[j + (size_t)n * c] = s;
-      }
+    host_stiefel_polar(Z.data(), r, n, Uk);
   }
 }
 
@@ -1170,6 +1176,165 @@ extern "C" int gpt_gmc(const double* phi, const double* y, int64_t n, int64_t D,
     for (int64_t z = 0; z < burnin + maxepoch; ++z) accept_prob[z] = std::nan("");
     set_error("Get NaN when moving along Geodesic. Try smaller epsU");
     return GPT_ERR_NAN_GEODESIC;
+  }
+  return GPT_OK;
+}
+
+// Non-cumulative epoch permutation randperm(N) on the PERM stream of `epoch` (the shuffles of
+// 100k_movielensExperiment.jl:451-452 permute the original ratings every epoch).
+static void host_randperm(int N, uint64_t seed, int epoch, int32_t* p) {
+  for (int i = 0; i < N; ++i) p[i] = i;
+  for (int i = N - 1; i >= 1; --i) {
+    const uint32_t x = philox4x32((uint32_t)i, (uint32_t)epoch, kPerm, 0, seed).x;
+    const int j = (int)(((uint64_t)x * (uint64_t)(i + 1)) >> 32);
+    std::swap(p[i], p[j]);
+  }
+}
+
+static void cf_features(const double* X, int n, int D, int rowbase, std::vector<int32_t>& ptr,
+                        std::vector<int32_t>& fe) {
+  ptr.assign((size_t)n + 1, 0);
+  fe.clear();
+  for (int i = 0; i < n; ++i) {
+    for (int f = 0; f < D; ++f)
+      if (X[i + (size_t)n * f] != 0.0) fe.push_back(rowbase + f);   // find(Data[i,:]) (:430-437)
+    ptr[i + 1] = (int32_t)fe.size();
+  }
+  if (fe.empty()) fe.push_back(0);
+}
+
+extern "C" int gpt_cf_fullw_sideinfo(
+    const double* Rating, int64_t N, int64_t ldr, const double* UserData, int64_t n1, int64_t D1,
+    const double* MovieData, int64_t n2, int64_t D2, const double* Ratingtest, int64_t Ntest,
+    int64_t ldt, double signal_var, double sigma_u, double sigma_w, const double* w_init, int64_t r,
+    int64_t m, double epsw, double epsU, double a, double b, double c, int64_t burnin,
+    int64_t maxepoch, uint64_t seed, double ytrainMean, double ytrainStd, int32_t langevin,
+    int32_t stiefel, int32_t avg, double* w_store, double* U_store, double* V_store,
+    double* testpred_store, double* trainRMSE, double* testRMSE) {
+  if (!Rating || !UserData || !MovieData || !Ratingtest || !w_init || !w_store || !U_store ||
+      !V_store || !testpred_store || !trainRMSE || !testRMSE || N < 1 || Ntest < 1 || ldr < N ||
+      ldt < Ntest || n1 < 1 || n2 < 1 || D1 < 0 || D2 < 0 || m < 1 || burnin < 0 || maxepoch < 0 ||
+      !(signal_var > 0) || !(sigma_u > 0) || !(sigma_w > 0)) {
+    set_error("bad GPT_fullw_sideinfo arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  if (!cf_rank_supported((int)r) || cf_lds_bytes((int)r, (int)m) > 160 * 1024) {
+    set_error("GPT_fullw_sideinfo: rank not instantiated (1-6,8,10,12,15,16,20) or minibatch too large");
+    return GPT_ERR_BAD_DIMS;
+  }
+  const int rowsU = (int)(n1 + D1), rowsV = (int)(n2 + D2);
+  std::vector<int32_t> tu(N), tm(N), eu(Ntest), em(Ntest);
+  std::vector<double> tr(N), er(Ntest);
+  for (int64_t i = 0; i < N; ++i) {
+    tu[i] = (int32_t)Rating[i] - 1; tm[i] = (int32_t)Rating[i + ldr] - 1; tr[i] = Rating[i + 2 * ldr];
+    if (tu[i] < 0 || tu[i] >= n1 || tm[i] < 0 || tm[i] >= n2) { set_error("rating ids out of range"); return GPT_ERR_BAD_DIMS; }
+  }
+  for (int64_t i = 0; i < Ntest; ++i) {
+    eu[i] = (int32_t)Ratingtest[i] - 1; em[i] = (int32_t)Ratingtest[i + ldt] - 1; er[i] = Ratingtest[i + 2 * ldt];
+    if (eu[i] < 0 || eu[i] >= n1 || em[i] < 0 || em[i] >= n2) { set_error("test rating ids out of range"); return GPT_ERR_BAD_DIMS; }
+  }
+  std::vector<int32_t> uptr, ufe, vptr, vfe;
+  cf_features(UserData, (int)n1, (int)D1, (int)n1, uptr, ufe);
+  cf_features(MovieData, (int)n2, (int)D2, (int)n2, vptr, vfe);
+  // U, V init (:424-428): Stiefel polar factor of Z = randn(r, rows) or sigma_u·randn(rows, r)
+  std::vector<double> U0((size_t)rowsU * r), V0((size_t)rowsV * r);
+  for (int which = 0; which < 2; ++which) {
+    const int rows = which ? rowsV : rowsU;
+    double* M = which ? V0.data() : U0.data();
+    std::vector<double> Z((size_t)rows * r);
+    for (size_t e = 0; e < Z.size(); ++e) Z[e] = host_normal(seed, (uint32_t)e, 0, kCfUVInit, (uint32_t)which);
+    if (stiefel) host_stiefel_polar(Z.data(), (int)r, rows, M);
+    else for (size_t e = 0; e < Z.size(); ++e) M[e] = sigma_u * Z[e];
+  }
+  const size_t nU = U0.size(), nV = V0.size(), rr = (size_t)r * r;
+  const int nbatch = (int)((N + m - 1) / m);
+  const int neval = (int)((std::max(N, Ntest) + 255) / 256);
+  DevMem d_tu, d_tm, d_tr, d_eu, d_em, d_er, d_up, d_uf, d_vp, d_vf, d_perm, d_w, d_U, d_V, d_GU,
+      d_GV, d_trp, d_tep, d_sse, d_st, d_ch;
+  HIPCHK(d_tu.alloc(4 * N)); HIPCHK(d_tm.alloc(4 * N)); HIPCHK(d_tr.alloc(8 * N));
+  HIPCHK(d_eu.alloc(4 * Ntest)); HIPCHK(d_em.alloc(4 * Ntest)); HIPCHK(d_er.alloc(8 * Ntest));
+  HIPCHK(d_up.alloc(4 * uptr.size())); HIPCHK(d_uf.alloc(4 * ufe.size()));
+  HIPCHK(d_vp.alloc(4 * vptr.size())); HIPCHK(d_vf.alloc(4 * vfe.size()));
+  HIPCHK(d_perm.alloc(4 * N)); HIPCHK(d_w.alloc(8 * rr)); HIPCHK(d_U.alloc(8 * nU));
+  HIPCHK(d_V.alloc(8 * nV)); HIPCHK(d_GU.alloc(8 * nU)); HIPCHK(d_GV.alloc(8 * nV));
+  HIPCHK(d_trp.alloc(8 * N)); HIPCHK(d_tep.alloc(8 * Ntest)); HIPCHK(d_sse.alloc(16 * (size_t)neval));
+  HIPCHK(d_st.alloc(4)); HIPCHK(d_ch.alloc(sizeof(CfChain)));
+  HIPCHK(hipMemcpy(d_tu.p, tu.data(), 4 * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_tm.p, tm.data(), 4 * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_tr.p, tr.data(), 8 * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_eu.p, eu.data(), 4 * Ntest, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_em.p, em.data(), 4 * Ntest, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_er.p, er.data(), 8 * Ntest, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_up.p, uptr.data(), 4 * uptr.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_uf.p, ufe.data(), 4 * ufe.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_vp.p, vptr.data(), 4 * vptr.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_vf.p, vfe.data(), 4 * vfe.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_w.p, w_init, 8 * rr, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_U.p, U0.data(), 8 * nU, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_V.p, V0.data(), 8 * nV, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(d_GU.p, 0, 8 * nU)); HIPCHK(hipMemset(d_GV.p, 0, 8 * nV));
+  HIPCHK(hipMemset(d_trp.p, 0, 8 * N)); HIPCHK(hipMemset(d_tep.p, 0, 8 * Ntest));
+  HIPCHK(hipMemset(d_st.p, 0, 4));
+  CfParams P{};
+  P.n1 = (int)n1; P.D1 = (int)D1; P.n2 = (int)n2; P.D2 = (int)D2; P.r = (int)r; P.m = (int)m;
+  P.rowsU = rowsU; P.rowsV = rowsV;
+  P.a = a; P.b = b; P.c = c; P.signal_var = signal_var; P.sigma_u = sigma_u; P.sigma_w = sigma_w;
+  P.epsw = epsw; P.epsU = epsU; P.langevin = langevin; P.stiefel = stiefel; P.seed = seed;
+  P.uptr = d_up.as<int32_t>(); P.ufe = d_uf.as<int32_t>(); P.vptr = d_vp.as<int32_t>(); P.vfe = d_vf.as<int32_t>();
+  CfChain C{};
+  C.tr_user = d_tu.as<int32_t>(); C.tr_movie = d_tm.as<int32_t>(); C.tr_rating = d_tr.as<double>();
+  C.te_user = d_eu.as<int32_t>(); C.te_movie = d_em.as<int32_t>(); C.te_rating = d_er.as<double>();
+  C.N = (int)N; C.Ntest = (int)Ntest; C.perm = d_perm.as<int32_t>();
+  C.w = d_w.as<double>(); C.U = d_U.as<double>(); C.V = d_V.as<double>();
+  C.GU = d_GU.as<double>(); C.GV = d_GV.as<double>();
+  C.trainpred = d_trp.as<double>(); C.testpred = d_tep.as<double>(); C.sse = d_sse.as<double>();
+  C.status = d_st.as<int32_t>();
+  HIPCHK(hipMemcpy(d_ch.p, &C, sizeof(CfChain), hipMemcpyHostToDevice));
+  std::memset(w_store, 0, 8 * rr * maxepoch);
+  std::memset(U_store, 0, 8 * nU * maxepoch);
+  std::memset(V_store, 0, 8 * nV * maxepoch);
+  std::memset(testpred_store, 0, 8 * (size_t)Ntest * maxepoch);
+  std::memset(trainRMSE, 0, 8 * (size_t)maxepoch);
+  for (int64_t z = 0; z < maxepoch; ++z) testRMSE[z] = 10.0;              // :441
+  std::vector<int32_t> perm(N);
+  std::vector<double> sse(2 * (size_t)neval), tp(Ntest);
+  int counter = 0, testcounter = 0;
+  for (int64_t epoch = 1; epoch <= burnin + maxepoch; ++epoch) {
+    host_randperm((int)N, seed, (int)(epoch - 1), perm.data());
+    HIPCHK(hipMemcpy(d_perm.p, perm.data(), 4 * N, hipMemcpyHostToDevice));
+    hipError_t e = launch_cf_epoch(P, d_ch.as<CfChain>(), 1, (epoch - 1) * nbatch, nbatch, nullptr);
+    if (e != hipSuccess) return hip_fail(e, "cf epoch kernel");
+    int32_t bad = 0;
+    HIPCHK(hipMemcpy(&bad, d_st.p, 4, hipMemcpyDeviceToHost));
+    if (bad) {                       // :490-492 — zero parameter stores, curves as they are
+      std::memset(w_store, 0, 8 * rr * maxepoch);
+      std::memset(U_store, 0, 8 * nU * maxepoch);
+      std::memset(V_store, 0, 8 * nV * maxepoch);
+      set_error("Get NaN when moving along Geodesic. Try smaller epsU");
+      return GPT_ERR_NAN_GEODESIC;
+    }
+    if (epoch > burnin) {
+      const int64_t s2 = epoch - burnin - 1;
+      HIPCHK(hipMemcpy(w_store + rr * s2, d_w.p, 8 * rr, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(U_store + nU * s2, d_U.p, 8 * nU, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(V_store + nV * s2, d_V.p, 8 * nV, hipMemcpyDeviceToHost));
+      if (!avg) counter = 0;
+      e = launch_cf_eval(P, d_ch.as<CfChain>(), 1, (int)std::max(N, Ntest), counter, ytrainMean,
+                         ytrainStd, nullptr);
+      if (e != hipSuccess) return hip_fail(e, "cf eval kernel");
+      HIPCHK(hipMemcpy(sse.data(), d_sse.p, 16 * (size_t)neval, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(tp.data(), d_tep.p, 8 * Ntest, hipMemcpyDeviceToHost));
+      double st0 = 0.0, st1 = 0.0;
+      for (int z = 0; z < neval; ++z) { st0 += sse[2 * z]; st1 += sse[2 * z + 1]; }
+      trainRMSE[s2] = std::sqrt(st0 / (double)N);
+      testRMSE[s2] = std::sqrt(st1 / (double)Ntest);
+      for (int64_t i = 0; i < Ntest; ++i)
+        testpred_store[(size_t)Ntest * s2 + i] = std::min(std::max(tp[i] * ytrainStd + ytrainMean, 1.0), 5.0);
+      counter += 1;
+      // :541-547 (the reference compares with the previous epoch's entry; none at s2 = 0)
+      if (epoch > 1 && s2 > 0 && testRMSE[s2] > testRMSE[s2 - 1]) testcounter += 1;
+      else testcounter = 0;
+    }
+    if (testcounter >= 5) break;
   }
   return GPT_OK;
 }

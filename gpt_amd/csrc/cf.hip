@@ -1,0 +1,405 @@
+// MovieLens-100k tensor collaborative filtering with side information (§8(f) item 1):
+// GPT_fullw_sideinfo, 100k_movielensExperiment.jl:409-551.
+//
+// Model: rating(user, movie) ≈ a · sumUᵀ w sumV with sumU = U[user] + b·Σ U[user's feature rows],
+// sumV = V[movie] + c·Σ V[movie's feature rows] (U: (n1+D1) × r, V: (n2+D2) × r, w: r × r).
+// One workgroup runs a whole epoch of one chain (fold): per minibatch the ratings' sums and
+// residuals are formed in LDS, the gradient rows (users / movies in the batch and their feature
+// rows) are summed in rating order — deterministic, no atomics — into zeroed dense gradient
+// buffers, and then every row of U and V takes its SGD / SGLD step (the prior term moves all
+// rows) or the Stiefel projection + geodesic.  A second kernel predicts every train / test
+// rating after the epoch (running averages, cutoff, squared errors per block).
+#include "device_util.h"
+
+namespace gpt {
+
+constexpr int kCfNT = 1024;
+constexpr int kCfNW = kCfNT / 64;
+
+// Sum of A[:, a]·B[:, b] over `rows` for every (a, b) < r², one wave per entry (wave sums).
+__device__ void cf_gram(const double* A, const double* B, int rows, int r, double* out) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int e = wv; e < r * r; e += kCfNW) {
+    const int a = e / r, b = e - a * r;
+    double s = 0.0;
+    for (int row = lane; row < rows; row += 64)
+      s = fma(gptr(A)[row + (size_t)rows * a], gptr(B)[row + (size_t)rows * b], s);
+    s = wave_sum(s);
+    if (lane == 0) out[e] = s;
+  }
+}
+
+// One U or V step (the update block of :481-507) on matrix M with gradient rows G (zeroed
+// afterwards).  which = 0 (U) / 1 (V) selects the noise stream.
+template <int R>
+__device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int which,
+                        long long step, double* scr) {
+  const int tid = threadIdx.x, wv = tid >> 6;
+  constexpr int RE = R + (R & 1);
+  const double sq = sqrt(P.epsU);
+  const uint32_t st = (uint32_t)step;
+  if (!P.stiefel) {
+    const double su2 = P.sigma_u * P.sigma_u;
+    for (int o = tid; o < rows * (RE / 2); o += kCfNT) {
+      const int row = o / (RE / 2), lp = o - row * (RE / 2);
+      double z[2] = {0.0, 0.0};
+      if (P.langevin)
+        normal_pair(P.seed, (uint32_t)((2 * lp + RE * row) >> 1), st, kCfUVNoise, (uint32_t)which,
+                    z[0], z[1]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int l = 2 * lp + h;
+        if (l >= R) break;
+        const size_t e = row + (size_t)rows * l;
+        const double m0 = gptr(M)[e];
+        double mn = m0 + P.epsU * (gptr(G)[e] - m0 / su2) / 2;
+        if (P.langevin) mn = mn + sq * z[h];
+        gptr_w(M)[e] = mn;
+        gptr_w(G)[e] = 0.0;
+      }
+    }
+    __syncthreads();
+    return true;
+  }
+  // Stiefel: mom = proj(M, √εU·G/2 [+ ξ]) (GPT_SGLD.jl:14-16), M = geod(M, mom, √εU) (:19-37)
+  constexpr int NN = 2 * R;
+  double* Mg = scr;                 // R²
+  double* Ag = Mg + R * R;          // R²
+  double* Sg = Ag + R * R;          // R²
+  double* X0 = Sg + R * R;          // 7 NN²
+  double* X1 = X0 + 7 * NN * NN;    // 7 R²
+  double* F = X1 + 7 * R * R;       // NN × R
+  double* nr = F + NN * R;          // R
+  int* flag = (int*)(nr + R);
+  for (int o = tid; o < rows * (RE / 2); o += kCfNT) {
+    const int row = o / (RE / 2), lp = o - row * (RE / 2);
+    double z[2] = {0.0, 0.0};
+    if (P.langevin)
+      normal_pair(P.seed, (uint32_t)((2 * lp + RE * row) >> 1), st, kCfUVNoise, (uint32_t)which,
+                  z[0], z[1]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int l = 2 * lp + h;
+      if (l >= R) break;
+      const size_t e = row + (size_t)rows * l;
+      gptr_w(G)[e] = sq * gptr(G)[e] / 2 + z[h];
+    }
+  }
+  if (tid == 0) flag[0] = 0;
+  __syncthreads();
+  cf_gram(M, G, rows, R, Mg);
+  __syncthreads();
+  for (int row = tid; row < rows; row += kCfNT) {
+    double x[R], u[R];
+#pragma unroll
+    for (int l = 0; l < R; ++l) {
+      u[l] = gptr(M)[row + (size_t)rows * l];
+      x[l] = gptr(G)[row + (size_t)rows * l];
+    }
+#pragma unroll
+    for (int bb = 0; bb < R; ++bb) {
+      double s = 0.0;
+#pragma unroll
+      for (int a2 = 0; a2 < R; ++a2) s = fma(u[a2], Mg[a2 * R + bb] + Mg[bb * R + a2], s);
+      gptr_w(G)[row + (size_t)rows * bb] = x[bb] - s / 2;
+    }
+  }
+  __syncthreads();
+  cf_gram(M, G, rows, R, Ag);
+  cf_gram(G, G, rows, R, Sg);
+  __syncthreads();
+  const double tt = sq;
+  if (wv == 0) {
+    for (int o = tid; o < NN * NN; o += 64) {
+      const int i = o / NN, j = o - i * NN;
+      double v;
+      if (i < R) v = j < R ? Ag[i * R + j] : -Sg[i * R + (j - R)];
+      else v = j < R ? (i - R == j ? 1.0 : 0.0) : Ag[(i - R) * R + (j - R)];
+      X0[o] = tt * v;
+    }
+    wave_sync();
+    if (wave_expm<NN>(X0) && tid == 0) flag[0] = 1;
+  } else if (wv == 1) {
+    const int ln = tid & 63;
+    for (int o = ln; o < R * R; o += 64) X1[o] = -tt * Ag[o];
+    wave_sync();
+    wave_expm<R>(X1);
+  }
+  __syncthreads();
+  if (flag[0]) return false;
+  const double* E = X0 + NN * NN;
+  const double* mx = X1 + R * R;
+  for (int o = tid; o < NN * R; o += kCfNT) {
+    const int a2 = o / R, l = o - a2 * R;
+    double s = 0.0;
+#pragma unroll
+    for (int c2 = 0; c2 < R; ++c2) s = fma(E[a2 * NN + c2], mx[c2 * R + l], s);
+    F[o] = s;
+  }
+  __syncthreads();
+  for (int row = tid; row < rows; row += kCfNT) {
+    double x[NN];
+#pragma unroll
+    for (int l = 0; l < R; ++l) {
+      x[l] = gptr(M)[row + (size_t)rows * l];
+      x[R + l] = gptr(G)[row + (size_t)rows * l];
+    }
+#pragma unroll
+    for (int l = 0; l < R; ++l) {
+      double s = 0.0;
+#pragma unroll
+      for (int a2 = 0; a2 < NN; ++a2) s = fma(x[a2], F[a2 * R + l], s);
+      gptr_w(M)[row + (size_t)rows * l] = s;
+      gptr_w(G)[row + (size_t)rows * l] = 0.0;
+    }
+  }
+  __syncthreads();
+  {
+    const int lane = tid & 63;
+    for (int l = wv; l < R; l += kCfNW) {
+      double s = 0.0;
+      for (int row = lane; row < rows; row += 64) {
+        const double v = gptr(M)[row + (size_t)rows * l];
+        s = fma(v, v, s);
+      }
+      s = wave_sum(s);
+      if (lane == 0) nr[l] = sqrt(s);
+    }
+  }
+  __syncthreads();
+  for (int o = tid; o < rows * R; o += kCfNT) {
+    const int l = o / rows;
+    gptr_w(M)[o] = gptr(M)[o] / nr[l];
+  }
+  __syncthreads();
+  return true;
+}
+
+template <int R>
+__global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfChain* chains,
+                                                         long long step0, int nb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const CfChain C = chains[blockIdx.x];
+  const int tid = threadIdx.x, m = P.m, N = C.N;
+  double* w_l = (double*)smem;                  // R²
+  double* wn_l = w_l + R * R;                   // R²
+  double* sU = wn_l + R * R;                    // m × R   sumU of each batch rating
+  double* sV = sU + (size_t)m * R;              // m × R
+  double* tU = sV + (size_t)m * R;              // m × R   sumU·w
+  double* tV = tU + (size_t)m * R;              // m × R   w·sumVᵀ
+  double* er = tV + (size_t)m * R;              // m       rating, then residual
+  int* us = (int*)(er + m);                     // m
+  int* ms = us + m;                             // m
+  double* scr = (double*)(ms + m);              // Stiefel scratch (2m ints keep 8-B alignment)
+  if (__hip_atomic_load(C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  for (int o = tid; o < R * R; o += kCfNT) w_l[o] = C.w[o];
+  const double is2 = 1.0 / P.signal_var;
+  for (int bt = 0; bt < nb; ++bt) {
+    const long long step = step0 + bt;
+    const int B = min(m, N - bt * m);
+    const double cN = (double)N / (double)B;
+    for (int ii = tid; ii < B; ii += kCfNT) {
+      const int idx = C.perm[bt * m + ii];
+      us[ii] = C.tr_user[idx];
+      ms[ii] = C.tr_movie[idx];
+      er[ii] = C.tr_rating[idx];
+    }
+    __syncthreads();
+    // sumU = U[user,:] + b·sum(U[uidx,:],1), sumV likewise (:462)
+    for (int o = tid; o < 2 * B * R; o += kCfNT) {
+      const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+      const double* M = side ? C.V : C.U;
+      const int rows = side ? P.rowsV : P.rowsU;
+      const int id = side ? ms[ii] : us[ii];
+      const int32_t* ptr = side ? P.vptr : P.uptr;
+      const int32_t* fe = side ? P.vfe : P.ufe;
+      double f = 0.0;
+      for (int z = ptr[id]; z < ptr[id + 1]; ++z) f += gptr(M)[fe[z] + (size_t)rows * l];
+      const double v = gptr(M)[id + (size_t)rows * l] + (side ? P.c : P.b) * f;
+      (side ? sV : sU)[ii * R + l] = v;
+    }
+    __syncthreads();
+    for (int o = tid; o < B * R; o += kCfNT) {
+      const int ii = o / R, j = o - ii * R;
+      double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        s1 = fma(sU[ii * R + i], w_l[i + R * j], s1);      // (sumU*w)[j]
+        s2 = fma(sV[ii * R + i], w_l[j + R * i], s2);      // (sumV*w')[j]
+      }
+      tU[ii * R + j] = s1;
+      tV[ii * R + j] = s2;
+    }
+    __syncthreads();
+    for (int ii = tid; ii < B; ii += kCfNT) {       // residual rating − a·sum((sumU*w).*sumV)
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < R; ++j) s = fma(tU[ii * R + j], sV[ii * R + j], s);
+      er[ii] = er[ii] - P.a * s;
+    }
+    __syncthreads();
+    // gradw (:466, :473-477) and the w step of :479-483 into wn
+    for (int o = tid; o < R * R; o += kCfNT) {
+      const int i = o % R, j = o / R;
+      double g = 0.0;
+      for (int ii = 0; ii < B; ++ii) g += er[ii] * (sU[ii * R + i] * sV[ii * R + j]) * is2;
+      const double G = g * cN - w_l[o] / (P.sigma_w * P.sigma_w);
+      double wn = w_l[o] + P.epsw * G / 2;
+      if (P.langevin)
+        wn = wn + sqrt(P.epsw) * normal_at(P.seed, (uint32_t)o, (uint32_t)step, kCfWNoise, 0);
+      wn_l[o] = wn;
+    }
+    // gradient rows in rating order (:467-471): the first rating of a user / movie in the batch
+    // sums its row; feature rows sum over the ratings whose user / movie carries them
+    for (int o = tid; o < 2 * B * R; o += kCfNT) {
+      const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+      const int* ids = side ? ms : us;
+      const int id = ids[ii];
+      bool first = true;
+      for (int z = 0; z < ii; ++z) first &= ids[z] != id;
+      if (!first) continue;
+      const double* T = side ? tU : tV;     // Vtemp = e·(sumU*w), Utemp = e·(sumV*w')
+      double g = 0.0;
+      for (int z = ii; z < B; ++z)
+        if (ids[z] == id) g += P.a * (er[z] * T[z * R + l]) * is2;
+      double* G = side ? C.GV : C.GU;
+      gptr_w(G)[id + (size_t)(side ? P.rowsV : P.rowsU) * l] = g * cN;
+    }
+    for (int o = tid; o < (P.D1 + P.D2) * R; o += kCfNT) {
+      const int side = o >= P.D1 * R ? 1 : 0;
+      const int x = side ? o - P.D1 * R : o, f = x / R, l = x - f * R;
+      const int* ids = side ? ms : us;
+      const int32_t* ptr = side ? P.vptr : P.uptr;
+      const int32_t* fe = side ? P.vfe : P.ufe;
+      const int row = (side ? P.n2 : P.n1) + f;
+      const double ab = P.a * (side ? P.c : P.b);
+      const double* T = side ? tU : tV;
+      double g = 0.0;
+      bool hit = false;
+      for (int z = 0; z < B; ++z) {
+        const int id = ids[z];
+        bool has = false;
+        for (int q = ptr[id]; q < ptr[id + 1]; ++q) has |= fe[q] == row;
+        if (has) { g += ab * (er[z] * T[z * R + l]) * is2; hit = true; }
+      }
+      if (hit) gptr_w(side ? C.GV : C.GU)[row + (size_t)(side ? P.rowsV : P.rowsU) * l] = g * cN;
+    }
+    __syncthreads();
+    if (!cf_move<R>(P, C.U, C.GU, P.rowsU, 0, step, scr) ||
+        !cf_move<R>(P, C.V, C.GV, P.rowsV, 1, step, scr)) {
+      if (tid == 0) __hip_atomic_store(C.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    for (int o = tid; o < R * R; o += kCfNT) w_l[o] = wn_l[o];
+    __syncthreads();
+  }
+  for (int o = tid; o < R * R; o += kCfNT) C.w[o] = w_l[o];
+}
+
+// Every train (blockIdx.y = 0) / test (1) rating of a chain: running average of a·sumUᵀw sumV
+// (:526-529, :536-539), de-standardised and cut off, squared error summed per block into
+// C.sse[2·blockIdx.x + set] (the host adds the partials in order).
+template <int R>
+__global__ __launch_bounds__(256) void cf_eval_kernel(CfParams P, const CfChain* chains, int counter,
+                                                      double ymean, double ystd) {
+  __shared__ double red[4];
+  const CfChain C = chains[blockIdx.z];
+  const int set = blockIdx.y;
+  const int n = set ? C.Ntest : C.N;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  double se = 0.0;
+  if (i < n) {
+    const int u = set ? C.te_user[i] : C.tr_user[i];
+    const int v = set ? C.te_movie[i] : C.tr_movie[i];
+    double su[R], sv[R];
+#pragma unroll
+    for (int l = 0; l < R; ++l) {
+      double f = 0.0;
+      for (int z = P.uptr[u]; z < P.uptr[u + 1]; ++z) f += C.U[P.ufe[z] + (size_t)P.rowsU * l];
+      su[l] = C.U[u + (size_t)P.rowsU * l] + P.b * f;
+      double g = 0.0;
+      for (int z = P.vptr[v]; z < P.vptr[v + 1]; ++z) g += C.V[P.vfe[z] + (size_t)P.rowsV * l];
+      sv[l] = C.V[v + (size_t)P.rowsV * l] + P.c * g;
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) t = fma(su[k], C.w[k + R * j], t);
+      s = fma(t, sv[j], s);
+    }
+    const double pred = P.a * s;
+    double* run = set ? C.testpred : C.trainpred;
+    const double avgp = (run[i] * counter + pred) / (counter + 1);
+    run[i] = avgp;
+    const double fin = fmin(fmax(avgp * ystd + ymean, 1.0), 5.0);
+    const double d = ystd * (set ? C.te_rating[i] : C.tr_rating[i]) + ymean - fin;
+    se = d * d;
+  }
+  se = wave_sum(se);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) red[wv] = se;
+  __syncthreads();
+  if (threadIdx.x == 0) C.sse[2 * blockIdx.x + set] = red[0] + red[1] + red[2] + red[3];
+}
+
+size_t cf_lds_bytes(int r, int m) {
+  const size_t base = 8 * (2 * (size_t)r * r + 4 * (size_t)m * r + m) + 4 * (2 * (size_t)m + 2);
+  const size_t nn = 2 * (size_t)r;
+  const size_t stf = 8 * (3 * (size_t)r * r + 7 * nn * nn + 7 * (size_t)r * r + nn * r + r) + 16;
+  return al16(base) + stf;
+}
+
+#define GPT_CF_RANKS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(15) X(16) X(20)
+
+bool cf_rank_supported(int r) {
+  switch (r) {
+#define CASE(RR) case RR:
+    GPT_CF_RANKS(CASE)
+#undef CASE
+    return true;
+    default: return false;
+  }
+}
+
+hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
+                           int nb, hipStream_t st) {
+  const size_t lds = cf_lds_bytes(P.r, P.m);
+  switch (P.r) {
+#define CASE(RR)                                                                              \
+  case RR: {                                                                                  \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      hipError_t e = hipFuncSetAttribute((const void*)cf_epoch_kernel<RR>,                     \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      if (e != hipSuccess) return e;                                                          \
+      attr = true;                                                                            \
+    }                                                                                         \
+    hipLaunchKernelGGL(cf_epoch_kernel<RR>, dim3(nchains), dim3(kCfNT), lds, st, P, chains,   \
+                       step0, nb);                                                            \
+  } break;
+    GPT_CF_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_cf_eval(const CfParams& P, const CfChain* chains, int nchains, int nmax,
+                          int counter, double ymean, double ystd, hipStream_t st) {
+  dim3 grid((unsigned)((nmax + 255) / 256), 2, nchains);
+  switch (P.r) {
+#define CASE(RR)                                                                              \
+  case RR:                                                                                    \
+    hipLaunchKernelGGL(cf_eval_kernel<RR>, grid, dim3(256), 0, st, P, chains, counter, ymean, \
+                       ystd);                                                                 \
+    break;
+    GPT_CF_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace gpt

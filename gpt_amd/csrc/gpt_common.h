@@ -16,7 +16,8 @@ enum Stream : uint32_t {
   kWInit = 1, kUInit = 2, kPerm = 3, kWNoise = 4, kUNoise = 5,
   kThetaInit = 6, kThetaNoise = 7, kSampleNZ = 8, kFeatZ = 9, kFeatB = 10,
   kTgpUInit = 11, kTgpI = 12, kTgpWNoise = 13, kTgpUNoise = 14,
-  kGmcP = 15, kGmcMom = 16, kGmcU = 17
+  kGmcP = 15, kGmcMom = 16, kGmcU = 17,
+  kCfUVInit = 18, kCfWNoise = 19, kCfUVNoise = 20
 };
 
 struct U4 { uint32_t x, y, z, w; };

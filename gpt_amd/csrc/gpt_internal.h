@@ -158,6 +158,44 @@ hipError_t launch_feature(const double* X, long long N, int D, const double* ls,
 hipError_t launch_feature_notensor(const double* X, long long N, int D, const double* ls,
                                    double c, const double* Z, const double* b, int n,
                                    double* phi, hipStream_t st);
+// MovieLens tensor CF (cf.hip, 100k_movielensExperiment.jl:409-551)
+struct CfParams {
+  int n1, D1, n2, D2, r, m, rowsU, rowsV;
+  double a, b, c, signal_var, sigma_u, sigma_w, epsw, epsU;
+  int langevin, stiefel;
+  uint64_t seed;
+  const int32_t* uptr;   // n1+1 CSR offsets into ufe: the feature rows (n1 + f) of each user
+  const int32_t* ufe;
+  const int32_t* vptr;   // n2+1
+  const int32_t* vfe;
+};
+
+struct CfChain {
+  const int32_t* tr_user;   // N   0-based ids
+  const int32_t* tr_movie;
+  const double* tr_rating;  // N   standardised
+  const int32_t* te_user;   // Ntest
+  const int32_t* te_movie;
+  const double* te_rating;
+  int N, Ntest;
+  const int32_t* perm;      // N   this epoch's permutation (0-based rows of the ratings)
+  double* w;                // r*r column-major
+  double* U;                // rowsU*r column-major
+  double* V;                // rowsV*r
+  double* GU;               // rowsU*r zeroed scratch (gradient rows / momentum)
+  double* GV;
+  double* trainpred;        // N      running averages (avg)
+  double* testpred;         // Ntest
+  double* sse;              // 2 * gridDim.x partial sums of the eval kernel
+  int32_t* status;
+};
+
+size_t cf_lds_bytes(int r, int m);
+bool cf_rank_supported(int r);
+hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
+                           int nb, hipStream_t st);
+hipError_t launch_cf_eval(const CfParams& P, const CfChain* chains, int nchains, int nmax,
+                          int counter, double ymean, double ystd, hipStream_t st);
 bool gmc_supported(int n, int r);
 hipError_t gmc_run(const double* phi, const double* y, const int32_t* I0, int n, int D,
                    long long N, int r, int Q, double signal_var, double epsw, double epsU,

@@ -1,0 +1,74 @@
+"""MovieLens-100k tensor collaborative filtering (100k_movielensExperiment.jl, §8(f) item 1 /
+BASELINE config 5) on libgptsgld.so.
+
+    GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w,
+                       w_init, m, epsw, epsU, a, b, c, burnin, maxepoch, param_seed,
+                       ytrainMean, ytrainStd; langevin=False, stiefel=False, avg=False)
+                                                             100k_movielensExperiment.jl:409-551
+    fold(data, i)     the standardised u{i}.base / u{i}.test split of :566-576
+
+Same argument meaning and return tuple as the reference: (w_store, U_store, V_store,
+testpred_store, trainRMSEvec, testRMSEvec).  ``data`` is the mapping written by
+scripts/make_ml100k_fixture.py (ratings per fold, the processed UserData / MovieData of
+:578-584).  Randomness follows the framework's Philox contract (oracle/movielens_ref.py).
+"""
+import numpy as np
+
+from ._lib import P_D, check, lib
+from . import _lib
+
+__all__ = ["GPT_fullw_sideinfo", "fold"]
+
+
+def _f64(a):
+    return np.asfortranarray(np.asarray(a, dtype=np.float64))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(P_D)
+
+
+def fold(data, i):
+    """(Ratingtrain, Ratingtest, UserData, MovieData, ytrainMean, ytrainStd) of fold i (1..5),
+    ratings standardised with the training mean / std (:570-575)."""
+    tr = np.asarray(data["u%d_base" % i], dtype=np.float64).copy()
+    te = np.asarray(data["u%d_test" % i], dtype=np.float64).copy()
+    mu, sd = tr[:, 2].mean(), tr[:, 2].std(ddof=1)
+    tr[:, 2] = (tr[:, 2] - mu) / sd
+    te[:, 2] = (te[:, 2] - mu) / sd
+    return (tr, te, np.asarray(data["user_data"], dtype=np.float64),
+            np.asarray(data["movie_data"], dtype=np.float64), mu, sd)
+
+
+def GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w,
+                       w_init, m, epsw, epsU, a, b, c, burnin, maxepoch, param_seed, ytrainMean,
+                       ytrainStd, langevin=False, stiefel=False, avg=False):
+    Rt = _f64(Rating)
+    Rs = _f64(Ratingtest)
+    Ud = _f64(UserData)
+    Md = _f64(MovieData)
+    w0 = _f64(w_init)
+    N, Ntest = Rt.shape[0], Rs.shape[0]
+    n1, D1 = Ud.shape
+    n2, D2 = Md.shape
+    r = w0.shape[0]
+    if Rt.shape[1] < 3 or Rs.shape[1] < 3 or w0.shape != (r, r):
+        raise ValueError("Rating / Ratingtest need (user, movie, rating) columns; w_init is r x r")
+    w_store = np.zeros((r, r, maxepoch), order="F")
+    U_store = np.zeros((n1 + D1, r, maxepoch), order="F")
+    V_store = np.zeros((n2 + D2, r, maxepoch), order="F")
+    tps = np.zeros((Ntest, maxepoch), order="F")
+    trm = np.zeros(maxepoch)
+    tsm = np.zeros(maxepoch)
+    code = lib().gpt_cf_fullw_sideinfo(
+        _ptr(Rt), N, N, _ptr(Ud), n1, D1, _ptr(Md), n2, D2, _ptr(Rs), Ntest, Ntest,
+        float(signal_var), float(sigma_u), float(sigma_w), _ptr(w0), r, int(m), float(epsw),
+        float(epsU), float(a), float(b), float(c), int(burnin), int(maxepoch),
+        int(param_seed) & (2 ** 64 - 1), float(ytrainMean), float(ytrainStd), int(bool(langevin)),
+        int(bool(stiefel)), int(bool(avg)), _ptr(w_store), _ptr(U_store), _ptr(V_store),
+        _ptr(tps), _ptr(trm), _ptr(tsm))
+    if code == _lib.GPT_ERR_NAN_GEODESIC:
+        print("Get NaN when moving along Geodesic. Try smaller epsU")
+    else:
+        check(code)
+    return w_store, U_store, V_store, tps, trm, tsm

@@ -205,6 +205,25 @@ int gpt_gmc(const double* phi, const double* y, int64_t n, int64_t D, int64_t N,
             int64_t burnin, int64_t maxepoch, int64_t L, uint64_t seed, const double* w_init,
             const double* U_init, double* w_store, double* U_store, double* accept_prob);
 
+/* ---- MovieLens-100k tensor CF with side information (§8(f) item 1, config 5) -------- */
+/* GPT_fullw_sideinfo(Rating,UserData,MovieData,Ratingtest,signal_var,sigma_u,sigma_w,w_init,m,
+ *   epsw,epsU,a,b,c,burnin,maxepoch,param_seed,ytrainMean,ytrainStd;langevin,stiefel,avg)
+ * 100k_movielensExperiment.jl:409-551.  Rating (N x >=3, leading dimension ldr, column-major):
+ * 1-based user, movie, standardised rating; Ratingtest likewise (ldt).  UserData (n1 x D1),
+ * MovieData (n2 x D2) column-major 0/1 side information; w_init (r x r).  Outputs (caller-
+ * allocated, column-major): w_store (r,r,maxepoch), U_store (n1+D1,r,maxepoch), V_store
+ * (n2+D2,r,maxepoch), testpred_store (Ntest,maxepoch), trainRMSE / testRMSE (maxepoch; epochs
+ * after the early stop of :545-547 keep 0 / 10).  GPT_ERR_NAN_GEODESIC: zero parameter stores. */
+int gpt_cf_fullw_sideinfo(const double* Rating, int64_t N, int64_t ldr, const double* UserData,
+                          int64_t n1, int64_t D1, const double* MovieData, int64_t n2, int64_t D2,
+                          const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var,
+                          double sigma_u, double sigma_w, const double* w_init, int64_t r, int64_t m,
+                          double epsw, double epsU, double a, double b, double c, int64_t burnin,
+                          int64_t maxepoch, uint64_t seed, double ytrainMean, double ytrainStd,
+                          int32_t langevin, int32_t stiefel, int32_t avg, double* w_store,
+                          double* U_store, double* V_store, double* testpred_store,
+                          double* trainRMSE, double* testRMSE);
+
 const char* gpt_last_error(void);
 /* LDS bytes one step workgroup needs for this shape (must be <= 163840). */
 int64_t gpt_sgld_lds_bytes(int64_t n, int64_t D, int64_t r, int64_t Q, int64_t m);

@@ -1,0 +1,155 @@
+"""CPU oracle for the MovieLens-100k tensor CF model (100k_movielensExperiment.jl, §8(f) item 1).
+
+TEST INFRASTRUCTURE — NOT PRODUCT CODE.  Only ``tests/`` may import this module; the product
+path (``gpt_amd.movielens`` + ``libgptsgld.so``) never touches ``oracle/``.
+
+``GPT_fullw_sideinfo`` restates 100k_movielensExperiment.jl:409-551 rating by rating, with the
+framework's Philox streams in place of Julia's MersenneTwister (oracle/philox.py):
+  * epoch permutation: ``randperm(N, seed, epoch-1)`` of the ORIGINAL ratings (:451-452 — not
+    cumulative, unlike GPTregression's ``phi=phi[:,:,perm]``);
+  * U, V init (:424-428): Stiefel polar factor of Z = randn(r, rows) with Z on (CF_UV_INIT, 0/1)
+    (element a + r·row), or sigma_u·randn(rows, r) on the same streams (element row + rows·l);
+  * noise: w on (step, CF_W_NOISE, 0) (element i + r·j), U/V on (step, CF_UV_NOISE, 0/1) in
+    u_noise's layout (element l + RE·row, RE = r rounded up to even).
+Row indices are 0-based here: user u -> U row u, user feature f -> U row n1 + f (Uidx, :430-437).
+"""
+import math
+
+import numpy as np
+
+from . import gpt_sgld_ref as R
+from . import philox as px
+
+
+def side_rows(user_data, movie_data):
+    """Uidx / Vidx of :430-437 (0-based rows of U and V)."""
+    n1, n2 = user_data.shape[0], movie_data.shape[0]
+    uidx = [n1 + np.flatnonzero(user_data[u]) for u in range(n1)]
+    vidx = [n2 + np.flatnonzero(movie_data[v]) for v in range(n2)]
+    return uidx, vidx
+
+
+def cutoff(pred):
+    """:49-52 — clamp predictions to [1, 5]."""
+    return np.clip(pred, 1.0, 5.0)
+
+
+def uv_noise(rows, r, seed, step, which):
+    re = r + (r & 1)
+    return px.normals(re * rows, seed, step, px.CF_UV_NOISE, which).reshape((rows, re))[:, :r]
+
+
+def init_uv(rows, r, seed, which, stiefel, sigma_u):
+    if stiefel:
+        z = px.normals(r * rows, seed, 0, px.CF_UV_INIT, which).reshape((r, rows), order="F")
+        return np.asfortranarray(R.stiefel_init(z))
+    return sigma_u * px.normals(rows * r, seed, 0, px.CF_UV_INIT, which).reshape((rows, r), order="F")
+
+
+def predict(ratings, U, V, w, uidx, vidx, a, b, c):
+    """a·sum((sumU*w).*sumV) for every (user, movie) row of ``ratings`` (:526-529)."""
+    out = np.empty(len(ratings))
+    for i, (u, v) in enumerate(ratings[:, :2].astype(np.int64) - 1):
+        sumU = U[u] + b * U[uidx[u]].sum(axis=0)
+        sumV = V[v] + c * V[vidx[v]].sum(axis=0)
+        out[i] = a * np.sum((sumU @ w) * sumV)
+    return out
+
+
+def GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w,
+                       w_init, m, epsw, epsU, a, b, c, burnin, maxepoch, param_seed, ytrainMean,
+                       ytrainStd, langevin=False, stiefel=False, avg=False):
+    """100k_movielensExperiment.jl:409-551.  Rating (N, 3+) holds 1-based user / movie ids and
+    the standardised rating.  Returns (w_store (r, r, T), U_store (n1+D1, r, T), V_store,
+    testpred_store (Ntest, T), trainRMSEvec (T), testRMSEvec (T)), T = maxepoch; entries of
+    epochs after an early stop (:545-547) stay 0 (10 for testRMSEvec, as :441)."""
+    Rating = np.asarray(Rating, dtype=np.float64)
+    Ratingtest = np.asarray(Ratingtest, dtype=np.float64)
+    N, Ntest = len(Rating), len(Ratingtest)
+    n1, D1 = UserData.shape
+    n2, D2 = MovieData.shape
+    nb = -(-N // m)
+    w = np.array(w_init, dtype=np.float64, order="F")
+    r = w.shape[0]
+    w_store = np.zeros((r, r, maxepoch), order="F")
+    U_store = np.zeros((n1 + D1, r, maxepoch), order="F")
+    V_store = np.zeros((n2 + D2, r, maxepoch), order="F")
+    testpred_store = np.zeros((Ntest, maxepoch), order="F")
+    U = init_uv(n1 + D1, r, param_seed, 0, stiefel, sigma_u)
+    V = init_uv(n2 + D2, r, param_seed, 1, stiefel, sigma_u)
+    uidx, vidx = side_rows(UserData, MovieData)
+    trainRMSE = np.zeros(maxepoch)
+    testRMSE = 10.0 * np.ones(maxepoch)
+    trainpred, testpred = np.zeros(N), np.zeros(Ntest)
+    counter = testcounter = 0
+    sq, sqw = math.sqrt(epsU), math.sqrt(epsw)
+    step = 0
+
+    def bail():
+        return (np.zeros_like(w_store), np.zeros_like(U_store), np.zeros_like(V_store),
+                testpred_store, trainRMSE, testRMSE)
+
+    for epoch in range(1, burnin + maxepoch + 1):
+        shuffled = Rating[px.randperm(N, param_seed, epoch - 1)]
+        for batch in range(nb):
+            br = shuffled[m * batch: min(m * (batch + 1), N)]
+            B = len(br)
+            gradw = np.zeros((r, r))
+            gradU = np.zeros((n1 + D1, r))
+            gradV = np.zeros((n2 + D2, r))
+            for ii in range(B):
+                u, v, rating = int(br[ii, 0]) - 1, int(br[ii, 1]) - 1, br[ii, 2]
+                sumU = U[u] + b * U[uidx[u]].sum(axis=0)
+                sumV = V[v] + c * V[vidx[v]].sum(axis=0)
+                t = sumU @ w
+                e = rating - a * np.sum(t * sumV)
+                Utemp = (e * sumV) @ w.T
+                Vtemp = (e * sumU) @ w
+                gradw += e * np.outer(sumU, sumV) / signal_var          # kron(sumV', sumU')
+                gradU[u] += a * Utemp / signal_var
+                gradV[v] += a * Vtemp / signal_var
+                gradU[uidx[u]] += a * b * Utemp / signal_var
+                gradV[vidx[v]] += a * c * Vtemp / signal_var
+            gradw = gradw * N / B - w / sigma_w ** 2
+            gradU *= N / B
+            gradV *= N / B
+            w = w + epsw * gradw / 2
+            if langevin:
+                w = w + sqw * px.normals(r * r, param_seed, step, px.CF_W_NOISE, 0).reshape((r, r), order="F")
+            new = []
+            for which, (M, G) in enumerate(((U, gradU), (V, gradV))):
+                xi = uv_noise(M.shape[0], r, param_seed, step, which)
+                if stiefel:
+                    mom = R.proj(M, sq * G / 2 + (xi if langevin else 0.0))
+                    Mn, ok = R.geod(M, mom, sq)
+                    if not ok:
+                        return bail()
+                else:
+                    Mn = M + epsU * (G - M / sigma_u ** 2) / 2
+                    if langevin:
+                        Mn = Mn + sq * xi
+                new.append(Mn)
+            U, V = new
+            step += 1
+        if epoch > burnin:
+            s = epoch - burnin - 1
+            w_store[:, :, s] = w
+            U_store[:, :, s] = U
+            V_store[:, :, s] = V
+            if not avg:
+                counter = 0
+            trainpred = (trainpred * counter + predict(Rating, U, V, w, uidx, vidx, a, b, c)) / (counter + 1)
+            ft = cutoff(trainpred * ytrainStd + ytrainMean)
+            trainRMSE[s] = math.sqrt(np.sum((ytrainStd * Rating[:, 2] + ytrainMean - ft) ** 2) / N)
+            testpred = (testpred * counter + predict(Ratingtest, U, V, w, uidx, vidx, a, b, c)) / (counter + 1)
+            fs = cutoff(testpred * ytrainStd + ytrainMean)
+            testpred_store[:, s] = fs
+            testRMSE[s] = math.sqrt(np.sum((ytrainStd * Ratingtest[:, 2] + ytrainMean - fs) ** 2) / Ntest)
+            counter += 1
+            if epoch > 1 and s > 0 and testRMSE[s] > testRMSE[s - 1]:
+                testcounter += 1
+            else:
+                testcounter = 0
+        if testcounter >= 5:
+            break
+    return w_store, U_store, V_store, testpred_store, trainRMSE, testRMSE

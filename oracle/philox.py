@@ -40,6 +40,8 @@ W_INIT, U_INIT, PERM, W_NOISE, U_NOISE, THETA_INIT, THETA_NOISE = 1, 2, 3, 4, 5,
 TGP_U_INIT, TGP_I, TGP_W_NOISE, TGP_U_NOISE = 11, 12, 13, 14
 # GPT_GMC (GPT_SGLD.jl:684-805): momentum of w, momentum of U, the accept/reject uniform
 GMC_P, GMC_MOM, GMC_U = 15, 16, 17
+# MovieLens tensor CF (100k_movielensExperiment.jl:409-551): U/V init, w noise, U/V noise
+CF_UV_INIT, CF_W_NOISE, CF_UV_NOISE = 18, 19, 20
 
 
 def philox4x32(c0, c1, c2, c3, seed):

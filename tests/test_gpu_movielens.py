@@ -1,0 +1,70 @@
+"""GPU parity of the MovieLens-100k tensor CF sampler (GPT_fullw_sideinfo,
+100k_movielensExperiment.jl:409-551; §8(f) item 1, BASELINE config 5) against the oracle.
+
+Data: the reference's ml-100k files as processed by :561-586 (tests/golden/ml100k.npz, built by
+scripts/make_ml100k_fixture.py).  Tolerances (fp64; the device sums gradient rows and feature
+sums in the reference's rating order but forms (e·sumV)·wᵀ as e·(sumV·wᵀ)):
+  w / U / V stores       max |Δ| <= 1e-8·max|x|
+  test predictions       max |Δ| <= 1e-8 (rating scale)
+  train / test RMSE      relative <= 1e-9
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import movielens_ref as M
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "ml100k.npz")
+
+
+def rel(a, b):
+    a = np.asarray(a); b = np.asarray(b)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+
+
+def problem(ntr, nte, fold=1):
+    from gpt_amd import movielens
+    d = np.load(GOLD)
+    tr, te, ud, md, mu, sd = movielens.fold(d, fold)
+    return tr[:ntr], te[:nte], ud, md, mu, sd
+
+
+CASES = {
+    # name: (ntrain, ntest, r, m, epochs, burnin, langevin, stiefel, avg, epsw, epsU)
+    "sgd_euclid_live": (3000, 1000, 4, 100, 2, 0, False, False, False, 1e-4, 1e-6),
+    "sgld_euclid_avg": (2950, 800, 5, 64, 3, 1, True, False, True, 1e-4, 1e-6),
+    "sgd_stiefel": (3000, 1000, 4, 100, 2, 0, False, True, False, 1e-4, 1e-4),
+    "sgld_stiefel": (2950, 800, 3, 64, 2, 0, True, True, True, 1e-4, 1e-4),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_fullw_sideinfo_matches_oracle(name):
+    from gpt_amd import movielens
+    ntr, nte, r, m, ep, bi, lang, stf, avg, epsw, epsU = CASES[name]
+    tr, te, ud, md, mu, sd = problem(ntr, nte)
+    w0 = np.random.default_rng(5).standard_normal((r, r))
+    args = (tr, ud, md, te, 0.8, 0.1, 1.0, w0, m, epsw, epsU, 0.5, 0.25, 0.5, bi, ep, 17, mu, sd)
+    got = movielens.GPT_fullw_sideinfo(*args, langevin=lang, stiefel=stf, avg=avg)
+    want = M.GPT_fullw_sideinfo(*args, langevin=lang, stiefel=stf, avg=avg)
+    for g, w_, tol in zip(got[:3], want[:3], (1e-8, 1e-8, 1e-8)):
+        assert rel(g, w_) < tol, rel(g, w_)
+    assert np.abs(got[3] - want[3]).max() < 1e-8
+    assert np.all(np.abs(got[4] - want[4]) <= 1e-9 * want[4])
+    assert np.all(np.abs(got[5] - want[5]) <= 1e-9 * want[5])
+
+
+def test_fullw_sideinfo_live_config_full_fold():
+    """The live run of :723-730 (r = 15, m = 100, SGD, a/b/c = 0.5/0.25/0.5) for one epoch of
+    fold 1 (80 000 ratings), against the oracle."""
+    from gpt_amd import movielens
+    tr, te, ud, md, mu, sd = problem(80000, 20000)
+    w0 = np.random.default_rng(17).standard_normal((15, 15))
+    args = (tr, ud, md, te, 0.8, 0.1, 1.0, w0, 100, 1e-4, 1e-6, 0.5, 0.25, 0.5, 0, 1, 17, mu, sd)
+    got = movielens.GPT_fullw_sideinfo(*args)
+    want = M.GPT_fullw_sideinfo(*args)
+    assert rel(got[0], want[0]) < 1e-8 and rel(got[1], want[1]) < 1e-8 and rel(got[2], want[2]) < 1e-8
+    assert abs(got[5][0] - want[5][0]) <= 1e-9 * want[5][0]
+    assert 0.8 < got[5][0] < 1.3                      # test RMSE on the 1..5 rating scale
