@@ -1338,3 +1338,195 @@ extern "C" int gpt_cf_fullw_sideinfo(
   }
   return GPT_OK;
 }
+
+// Q of a Householder QR (LAPACK dgeqr2 + dorg2r conventions), r × r column-major in place.
+static void host_qr_q(int r, std::vector<double>& A) {
+  std::vector<double> tau(r, 0.0);
+  for (int k = 0; k < r; ++k) {
+    double xn = 0.0;
+    for (int i = k + 1; i < r; ++i) xn = std::hypot(xn, A[i + (size_t)r * k]);
+    const double alpha = A[k + (size_t)r * k];
+    if (xn == 0.0) { tau[k] = 0.0; continue; }
+    const double beta = -std::copysign(std::hypot(alpha, xn), alpha);
+    tau[k] = (beta - alpha) / beta;
+    const double sc = 1.0 / (alpha - beta);
+    for (int i = k + 1; i < r; ++i) A[i + (size_t)r * k] *= sc;
+    A[k + (size_t)r * k] = beta;
+    for (int j = k + 1; j < r; ++j) {            // apply H_k to the trailing columns
+      double s = A[k + (size_t)r * j];
+      for (int i = k + 1; i < r; ++i) s += A[i + (size_t)r * k] * A[i + (size_t)r * j];
+      s *= tau[k];
+      A[k + (size_t)r * j] -= s;
+      for (int i = k + 1; i < r; ++i) A[i + (size_t)r * j] -= s * A[i + (size_t)r * k];
+    }
+  }
+  std::vector<double> Qm((size_t)r * r, 0.0);
+  for (int i = 0; i < r; ++i) Qm[i + (size_t)r * i] = 1.0;
+  for (int k = r - 1; k >= 0; --k) {             // Q = H_0 … H_{r-1} applied to I (dorg2r)
+    for (int j = k; j < r; ++j) {
+      double s = Qm[k + (size_t)r * j];
+      for (int i = k + 1; i < r; ++i) s += A[i + (size_t)r * k] * Qm[i + (size_t)r * j];
+      s *= tau[k];
+      Qm[k + (size_t)r * j] -= s;
+      for (int i = k + 1; i < r; ++i) Qm[i + (size_t)r * j] -= s * A[i + (size_t)r * k];
+    }
+  }
+  A.swap(Qm);
+}
+
+extern "C" int gpt_cf_fullw_gibbs(
+    const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2, const double* Ratingtest,
+    int64_t Ntest, int64_t ldt, double signal_var, double sigma_u, double sigma_w,
+    const double* w_init, int64_t r, int64_t burnin, int64_t maxepoch, int64_t n_samples,
+    uint64_t seed, double ytrainMean, double ytrainStd, int32_t avg, int32_t rotated_w,
+    double* w_store, double* U_store, double* V_store, double* testpred_store, double* trainRMSE,
+    double* testRMSE) {
+  if (!Rating || !Ratingtest || !w_init || !w_store || !U_store || !V_store || !testpred_store ||
+      !trainRMSE || !testRMSE || N < 1 || Ntest < 1 || ldr < N || ldt < Ntest || n1 < 1 || n2 < 1 ||
+      burnin < 0 || maxepoch < 0 || n_samples < 1 || !(signal_var > 0) || !(sigma_u > 0) ||
+      !(sigma_w > 0)) {
+    set_error("bad GPT_fullw_gibbs arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  if (!cf_rank_supported((int)r) || r * r > 1024) {
+    set_error("GPT_fullw_gibbs: rank not instantiated (1-6,8,10,12,15,16,20)"); return GPT_ERR_BAD_DIMS;
+  }
+  std::vector<int32_t> tu(N), tm(N), eu(Ntest), em(Ntest);
+  std::vector<double> tr(N), er(Ntest);
+  for (int64_t i = 0; i < N; ++i) {
+    tu[i] = (int32_t)Rating[i] - 1; tm[i] = (int32_t)Rating[i + ldr] - 1; tr[i] = Rating[i + 2 * ldr];
+    if (tu[i] < 0 || tu[i] >= n1 || tm[i] < 0 || tm[i] >= n2) { set_error("rating ids out of range"); return GPT_ERR_BAD_DIMS; }
+  }
+  for (int64_t i = 0; i < Ntest; ++i) {
+    eu[i] = (int32_t)Ratingtest[i] - 1; em[i] = (int32_t)Ratingtest[i + ldt] - 1; er[i] = Ratingtest[i + 2 * ldt];
+    if (eu[i] < 0 || eu[i] >= n1 || em[i] < 0 || em[i] >= n2) { set_error("test rating ids out of range"); return GPT_ERR_BAD_DIMS; }
+  }
+  // ratings of each user / movie in Rating order (idx = (Rating[:,1].==i), :1061)
+  std::vector<int32_t> uptr(n1 + 1, 0), mptr(n2 + 1, 0), ulst(N), mlst(N);
+  for (int64_t i = 0; i < N; ++i) { uptr[tu[i] + 1]++; mptr[tm[i] + 1]++; }
+  for (int64_t i = 0; i < n1; ++i) uptr[i + 1] += uptr[i];
+  for (int64_t i = 0; i < n2; ++i) mptr[i + 1] += mptr[i];
+  {
+    std::vector<int32_t> cu(uptr.begin(), uptr.end() - 1), cm(mptr.begin(), mptr.end() - 1);
+    for (int64_t i = 0; i < N; ++i) { ulst[cu[tu[i]]++] = (int32_t)i; mlst[cm[tm[i]]++] = (int32_t)i; }
+  }
+  // init (:1047-1053): Q = qr(randn(r,r)), U = σ_u·randn(n1,r), V = σ_u·randn(n2,r)
+  const size_t rr = (size_t)r * r, nU = (size_t)n1 * r, nV = (size_t)n2 * r;
+  std::vector<double> Qm(rr), U0(nU), V0(nV), w0(w_init, w_init + rr);
+  for (size_t e = 0; e < rr; ++e) Qm[e] = host_normal(seed, (uint32_t)e, 0, kCfgInit, 0);
+  for (size_t e = 0; e < nU; ++e) U0[e] = sigma_u * host_normal(seed, (uint32_t)e, 0, kCfgInit, 1);
+  for (size_t e = 0; e < nV; ++e) V0[e] = sigma_u * host_normal(seed, (uint32_t)e, 0, kCfgInit, 2);
+  host_qr_q((int)r, Qm);
+  if (rotated_w) {                                // w = Q·w_init; U = U·Q'
+    for (int64_t i = 0; i < r; ++i)
+      for (int64_t j = 0; j < r; ++j) {
+        double s = 0.0;
+        for (int64_t k = 0; k < r; ++k) s += Qm[i + r * k] * w_init[k + r * j];
+        w0[i + r * j] = s;
+      }
+    std::vector<double> U1(nU);
+    for (int64_t i = 0; i < n1; ++i)
+      for (int64_t j = 0; j < r; ++j) {
+        double s = 0.0;
+        for (int64_t k = 0; k < r; ++k) s += U0[i + n1 * k] * Qm[j + r * k];
+        U1[i + n1 * j] = s;
+      }
+    U0.swap(U1);
+  }
+  const int p = (int)rr;
+  const int neval = (int)((std::max(N, Ntest) + 255) / 256);
+  DevMem d_tu, d_tm, d_tr, d_eu, d_em, d_er, d_up, d_mp, d_ul, d_ml, d_w, d_U, d_V, d_A, d_M, d_x,
+      d_z, d_trp, d_tep, d_sse, d_st, d_ch, d_zu, d_zv;
+  HIPCHK(d_tu.alloc(4 * N)); HIPCHK(d_tm.alloc(4 * N)); HIPCHK(d_tr.alloc(8 * N));
+  HIPCHK(d_eu.alloc(4 * Ntest)); HIPCHK(d_em.alloc(4 * Ntest)); HIPCHK(d_er.alloc(8 * Ntest));
+  HIPCHK(d_up.alloc(4 * uptr.size())); HIPCHK(d_mp.alloc(4 * mptr.size()));
+  HIPCHK(d_ul.alloc(4 * N)); HIPCHK(d_ml.alloc(4 * N));
+  HIPCHK(d_w.alloc(8 * rr)); HIPCHK(d_U.alloc(8 * nU)); HIPCHK(d_V.alloc(8 * nV));
+  HIPCHK(d_A.alloc(8 * rr * N)); HIPCHK(d_M.alloc(8 * rr * rr)); HIPCHK(d_x.alloc(8 * rr));
+  HIPCHK(d_z.alloc(8 * rr)); HIPCHK(d_trp.alloc(8 * N)); HIPCHK(d_tep.alloc(8 * Ntest));
+  HIPCHK(d_sse.alloc(16 * (size_t)neval)); HIPCHK(d_st.alloc(4)); HIPCHK(d_ch.alloc(sizeof(CfChain)));
+  HIPCHK(d_zu.alloc(4 * (n1 + 1))); HIPCHK(d_zv.alloc(4 * (n2 + 1)));
+  HIPCHK(hipMemcpy(d_tu.p, tu.data(), 4 * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_tm.p, tm.data(), 4 * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_tr.p, tr.data(), 8 * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_eu.p, eu.data(), 4 * Ntest, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_em.p, em.data(), 4 * Ntest, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_er.p, er.data(), 8 * Ntest, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_up.p, uptr.data(), 4 * uptr.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_mp.p, mptr.data(), 4 * mptr.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_ul.p, ulst.data(), 4 * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_ml.p, mlst.data(), 4 * N, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_w.p, w0.data(), 8 * rr, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_U.p, U0.data(), 8 * nU, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_V.p, V0.data(), 8 * nV, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(d_trp.p, 0, 8 * N)); HIPCHK(hipMemset(d_tep.p, 0, 8 * Ntest));
+  HIPCHK(hipMemset(d_st.p, 0, 4));
+  HIPCHK(hipMemset(d_zu.p, 0, 4 * (n1 + 1))); HIPCHK(hipMemset(d_zv.p, 0, 4 * (n2 + 1)));
+  // prediction without side information: a = 1, b = c = 0, empty feature lists (:1101-1102)
+  CfParams P{};
+  P.n1 = (int)n1; P.D1 = 0; P.n2 = (int)n2; P.D2 = 0; P.r = (int)r; P.m = 1;
+  P.rowsU = (int)n1; P.rowsV = (int)n2; P.a = 1.0; P.b = 0.0; P.c = 0.0;
+  P.signal_var = signal_var; P.sigma_u = sigma_u; P.sigma_w = sigma_w; P.seed = seed;
+  P.uptr = d_zu.as<int32_t>(); P.ufe = d_zu.as<int32_t>(); P.vptr = d_zv.as<int32_t>(); P.vfe = d_zv.as<int32_t>();
+  CfChain Cc{};
+  Cc.tr_user = d_tu.as<int32_t>(); Cc.tr_movie = d_tm.as<int32_t>(); Cc.tr_rating = d_tr.as<double>();
+  Cc.te_user = d_eu.as<int32_t>(); Cc.te_movie = d_em.as<int32_t>(); Cc.te_rating = d_er.as<double>();
+  Cc.N = (int)N; Cc.Ntest = (int)Ntest; Cc.w = d_w.as<double>(); Cc.U = d_U.as<double>();
+  Cc.V = d_V.as<double>(); Cc.trainpred = d_trp.as<double>(); Cc.testpred = d_tep.as<double>();
+  Cc.sse = d_sse.as<double>(); Cc.status = d_st.as<int32_t>();
+  HIPCHK(hipMemcpy(d_ch.p, &Cc, sizeof(CfChain), hipMemcpyHostToDevice));
+  std::memset(w_store, 0, 8 * rr * maxepoch);
+  std::memset(U_store, 0, 8 * nU * maxepoch);
+  std::memset(V_store, 0, 8 * nV * maxepoch);
+  std::memset(testpred_store, 0, 8 * (size_t)Ntest * maxepoch);
+  std::memset(trainRMSE, 0, 8 * (size_t)maxepoch);
+  std::memset(testRMSE, 0, 8 * (size_t)maxepoch);
+  const double su2 = sigma_u * sigma_u;
+  std::vector<double> sse(2 * (size_t)neval), tp(Ntest);
+  int counter = 0;
+  uint32_t sweep = 0;
+  for (int64_t epoch = 1; epoch <= burnin + maxepoch; ++epoch) {
+    for (int64_t g = 0; g < n_samples; ++g, ++sweep) {
+      hipError_t e = launch_cfg_rows(0, (int)r, d_w.as<double>(), d_V.as<double>(), (int)n2,
+                                     d_U.as<double>(), (int)n1, d_up.as<int32_t>(), d_ul.as<int32_t>(),
+                                     d_tm.as<int32_t>(), d_tr.as<double>(), signal_var, su2, seed,
+                                     sweep, kCfgU, d_st.as<int32_t>(), nullptr);
+      if (e == hipSuccess)
+        e = launch_cfg_rows(1, (int)r, d_w.as<double>(), d_U.as<double>(), (int)n1, d_V.as<double>(),
+                            (int)n2, d_mp.as<int32_t>(), d_ml.as<int32_t>(), d_tu.as<int32_t>(),
+                            d_tr.as<double>(), signal_var, su2, seed, sweep, kCfgV,
+                            d_st.as<int32_t>(), nullptr);
+      if (e == hipSuccess)
+        e = launch_cfg_kron((int)r, d_U.as<double>(), (int)n1, d_V.as<double>(), (int)n2,
+                            d_tu.as<int32_t>(), d_tm.as<int32_t>(), (int)N, d_A.as<double>(), nullptr);
+      if (e == hipSuccess)
+        e = gaussian_draw_dense(d_A.as<double>(), p, N, d_tr.as<double>(), 1.0 / signal_var,
+                                1.0 / (sigma_w * sigma_w), 1.0 / signal_var, seed, sweep, kCfgW, 0,
+                                d_M.as<double>(), d_x.as<double>(), d_z.as<double>(),
+                                d_w.as<double>(), d_st.as<int32_t>(), nullptr);
+      if (e != hipSuccess) return hip_fail(e, "GPT_fullw_gibbs sweep");
+    }
+    int32_t bad = 0;
+    HIPCHK(hipMemcpy(&bad, d_st.p, 4, hipMemcpyDeviceToHost));
+    if (bad) { set_error("PosDefException: a Gibbs precision matrix is not positive definite"); return GPT_ERR_NOT_SPD; }
+    if (epoch > burnin) {
+      const int64_t s2 = epoch - burnin - 1;
+      HIPCHK(hipMemcpy(w_store + rr * s2, d_w.p, 8 * rr, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(U_store + nU * s2, d_U.p, 8 * nU, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(V_store + nV * s2, d_V.p, 8 * nV, hipMemcpyDeviceToHost));
+      if (!avg) counter = 0;
+      hipError_t e = launch_cf_eval(P, d_ch.as<CfChain>(), 1, (int)std::max(N, Ntest), counter,
+                                    ytrainMean, ytrainStd, nullptr);
+      if (e != hipSuccess) return hip_fail(e, "cf eval kernel");
+      HIPCHK(hipMemcpy(sse.data(), d_sse.p, 16 * (size_t)neval, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(tp.data(), d_tep.p, 8 * Ntest, hipMemcpyDeviceToHost));
+      double st0 = 0.0, st1 = 0.0;
+      for (int z = 0; z < neval; ++z) { st0 += sse[2 * z]; st1 += sse[2 * z + 1]; }
+      trainRMSE[s2] = std::sqrt(st0 / (double)N);
+      testRMSE[s2] = std::sqrt(st1 / (double)Ntest);
+      for (int64_t i = 0; i < Ntest; ++i)
+        testpred_store[(size_t)Ntest * s2 + i] = std::min(std::max(tp[i] * ytrainStd + ytrainMean, 1.0), 5.0);
+      counter += 1;
+    }
+  }
+  return GPT_OK;
+}

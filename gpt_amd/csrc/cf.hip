@@ -13,6 +13,8 @@
 
 namespace gpt {
 
+#define GPT_CF_RANKS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(15) X(16) X(20)
+
 constexpr int kCfNT = 1024;
 constexpr int kCfNW = kCfNT / 64;
 
@@ -344,6 +346,151 @@ __global__ __launch_bounds__(256) void cf_eval_kernel(CfParams P, const CfChain*
   if (threadIdx.x == 0) C.sse[2 * blockIdx.x + set] = red[0] + red[1] + red[2] + red[3];
 }
 
+// ============================================================================ GPT_fullw_gibbs
+// 100k_movielensExperiment.jl:1032-1129.  One wave per user (side 0) / movie (side 1): the
+// conditional of its row given the other side and w — X = V[Ni,:]·wᵀ (users) or U[Nj,:]·w
+// (movies) streamed rating by rating, precision XᵀX/σ² + I/σ_u², in-wave Cholesky, row =
+// chol(·,:U) \ z + (precision \ Xᵀy)/σ² (:1063-1070, :1077-1084).  status = 1: not SPD.
+template <int R>
+__global__ __launch_bounds__(256) void cfg_rows_kernel(int side, const double* __restrict__ W,
+                                                       const double* __restrict__ Oth, int rows_oth,
+                                                       double* __restrict__ Me, int rows_me,
+                                                       const int32_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ lst,
+                                                       const int32_t* __restrict__ other,
+                                                       const double* __restrict__ y,
+                                                       double signal_var, double su2,
+                                                       uint64_t seed, uint32_t sweep,
+                                                       uint32_t stream, int32_t* __restrict__ status) {
+  constexpr int NE = (R * R + 63) / 64;
+  __shared__ double Ls[4][R * R], xs[4][R], rh[4][R], zs[4][R];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ent = blockIdx.x * 4 + wv;
+  if (ent >= rows_me) return;                       // whole waves only: no block barriers below
+  const int z0 = ptr[ent], z1 = ptr[ent + 1];
+  if (z0 == z1) return;                             // no ratings: the row is left as it is
+  double* A = Ls[wv];
+  double* x = xs[wv];
+  double acc[NE];
+#pragma unroll
+  for (int t = 0; t < NE; ++t) acc[t] = 0.0;
+  double racc = 0.0;
+  for (int z = z0; z < z1; ++z) {
+    const int ri = lst[z], o = other[ri];
+    if (lane < R) {
+      double s2 = 0.0;
+      if (side == 0) {
+#pragma unroll
+        for (int b = 0; b < R; ++b) s2 = fma(Oth[o + (size_t)rows_oth * b], W[lane + R * b], s2);
+      } else {
+#pragma unroll
+        for (int a = 0; a < R; ++a) s2 = fma(Oth[o + (size_t)rows_oth * a], W[a + R * lane], s2);
+      }
+      x[lane] = s2;
+    }
+    wave_sync();
+#pragma unroll
+    for (int t = 0; t < NE; ++t) {
+      const int e = lane + 64 * t;
+      if (e < R * R) acc[t] = fma(x[e % R], x[e / R], acc[t]);
+    }
+    if (lane < R) racc = fma(x[lane], y[ri], racc);
+    wave_sync();
+  }
+#pragma unroll
+  for (int t = 0; t < NE; ++t) {
+    const int e = lane + 64 * t;
+    if (e < R * R) A[e] = acc[t] / signal_var + ((e % R) == (e / R) ? 1.0 / su2 : 0.0);
+  }
+  if (lane < R) {
+    rh[wv][lane] = racc;
+    zs[wv][lane] = normal_at(seed, (uint32_t)lane, sweep, stream, (uint32_t)ent);
+  }
+  wave_sync();
+  bool bad = false;
+  for (int j = 0; j < R; ++j) {                     // lower Cholesky in place (A[i + R·k], i >= k)
+    const double d = A[j + R * j];
+    bad |= !(d > 0.0);
+    const double pv = sqrt(d);
+    wave_sync();
+    if (lane == 0) A[j + R * j] = pv;
+    if (lane > j && lane < R) A[lane + R * j] /= pv;
+    wave_sync();
+    for (int e = lane; e < R * R; e += 64) {
+      const int i = e % R, k = e / R;
+      if (k > j && i >= k) A[i + R * k] -= A[i + R * j] * A[k + R * j];
+    }
+    wave_sync();
+  }
+  if (lane == 0) {
+    if (bad) *status = 1;
+    double* rb = rh[wv];
+    double* zb = zs[wv];
+    for (int i = 0; i < R; ++i) {                   // L⁻¹ rhs
+      double s2 = rb[i];
+      for (int k = 0; k < i; ++k) s2 -= A[i + R * k] * rb[k];
+      rb[i] = s2 / A[i + R * i];
+    }
+    for (int i = R - 1; i >= 0; --i) {              // L⁻ᵀ (L⁻¹ rhs) and L⁻ᵀ z
+      double s2 = rb[i], s3 = zb[i];
+      for (int k = i + 1; k < R; ++k) {
+        s2 -= A[k + R * i] * rb[k];
+        s3 -= A[k + R * i] * zb[k];
+      }
+      rb[i] = s2 / A[i + R * i];
+      zb[i] = s3 / A[i + R * i];
+    }
+    for (int a = 0; a < R; ++a) Me[ent + (size_t)rows_me * a] = zb[a] + rb[a] / signal_var;
+  }
+}
+
+// Kron[:, i] = kron(V[movie_i,:], U[user_i,:]) as the r² × N design of w (:1087-1090).
+template <int R>
+__global__ void cfg_kron_kernel(const double* __restrict__ U, int n1, const double* __restrict__ V,
+                                int n2, const int32_t* __restrict__ users,
+                                const int32_t* __restrict__ movies, int N, double* __restrict__ A) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)R * R * N) return;
+  const int i = (int)(e / (R * R)), lk = (int)(e - (long long)i * R * R), l = lk % R, k = lk / R;
+  A[e] = V[movies[i] + (size_t)n2 * k] * U[users[i] + (size_t)n1 * l];
+}
+
+hipError_t launch_cfg_rows(int side, int r, const double* W, const double* Oth, int rows_oth,
+                           double* Me, int rows_me, const int32_t* ptr, const int32_t* lst,
+                           const int32_t* other, const double* y, double signal_var, double su2,
+                           uint64_t seed, uint32_t sweep, uint32_t stream, int32_t* status,
+                           hipStream_t st) {
+  switch (r) {
+#define CASE(RR)                                                                              \
+  case RR:                                                                                    \
+    hipLaunchKernelGGL(cfg_rows_kernel<RR>, dim3((rows_me + 3) / 4), dim3(256), 0, st, side, W, \
+                       Oth, rows_oth, Me, rows_me, ptr, lst, other, y, signal_var, su2, seed,  \
+                       sweep, stream, status);                                                \
+    break;
+    GPT_CF_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_cfg_kron(int r, const double* U, int n1, const double* V, int n2,
+                           const int32_t* users, const int32_t* movies, int N, double* A,
+                           hipStream_t st) {
+  const long long tot = (long long)r * r * N;
+  switch (r) {
+#define CASE(RR)                                                                              \
+  case RR:                                                                                    \
+    hipLaunchKernelGGL(cfg_kron_kernel<RR>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, \
+                       st, U, n1, V, n2, users, movies, N, A);                                \
+    break;
+    GPT_CF_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 size_t cf_lds_bytes(int r, int m) {
   const size_t base = 8 * (2 * (size_t)r * r + 4 * (size_t)m * r + m) + 4 * (2 * (size_t)m + 2);
   const size_t nn = 2 * (size_t)r;
@@ -351,7 +498,6 @@ size_t cf_lds_bytes(int r, int m) {
   return al16(base) + stf;
 }
 
-#define GPT_CF_RANKS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(15) X(16) X(20)
 
 bool cf_rank_supported(int r) {
   switch (r) {

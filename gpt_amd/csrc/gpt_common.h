@@ -17,7 +17,8 @@ enum Stream : uint32_t {
   kThetaInit = 6, kThetaNoise = 7, kSampleNZ = 8, kFeatZ = 9, kFeatB = 10,
   kTgpUInit = 11, kTgpI = 12, kTgpWNoise = 13, kTgpUNoise = 14,
   kGmcP = 15, kGmcMom = 16, kGmcU = 17,
-  kCfUVInit = 18, kCfWNoise = 19, kCfUVNoise = 20
+  kCfUVInit = 18, kCfWNoise = 19, kCfUVNoise = 20,
+  kCfgInit = 21, kCfgU = 22, kCfgV = 23, kCfgW = 24
 };
 
 struct U4 { uint32_t x, y, z, w; };

@@ -196,6 +196,18 @@ hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains
                            int nb, hipStream_t st);
 hipError_t launch_cf_eval(const CfParams& P, const CfChain* chains, int nchains, int nmax,
                           int counter, double ymean, double ystd, hipStream_t st);
+hipError_t launch_cfg_rows(int side, int r, const double* W, const double* Oth, int rows_oth,
+                           double* Me, int rows_me, const int32_t* ptr, const int32_t* lst,
+                           const int32_t* other, const double* y, double signal_var, double su2,
+                           uint64_t seed, uint32_t sweep, uint32_t stream, int32_t* status,
+                           hipStream_t st);
+hipError_t launch_cfg_kron(int r, const double* U, int n1, const double* V, int n2,
+                           const int32_t* users, const int32_t* movies, int N, double* A,
+                           hipStream_t st);
+hipError_t gaussian_draw_dense(const double* A, int p, long long N, const double* y, double alpha,
+                               double beta, double ysc, uint64_t seed, uint32_t c1, uint32_t c2,
+                               uint32_t c3, double* M, double* x, double* z, double* out,
+                               int32_t* status, hipStream_t st);
 bool gmc_supported(int n, int r);
 hipError_t gmc_run(const double* phi, const double* y, const int32_t* I0, int n, int D,
                    long long N, int r, int Q, double signal_var, double epsw, double epsU,

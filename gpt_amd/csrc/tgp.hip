@@ -145,6 +145,12 @@ __global__ void axpy_kernel(double* __restrict__ x, const double* __restrict__ z
   if (a < p) x[a] += z[a];
 }
 
+__global__ void gmc_sum_kernel(const double* __restrict__ a, const double* __restrict__ b,
+                               double* __restrict__ out, int p) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < p) out[e] = a[e] + b[e];
+}
+
 // z[e] = element e of Philox normal stream (c1, c2, c3)
 __global__ void normals_kernel(double* __restrict__ z, int cnt, uint64_t seed, uint32_t c1,
                                uint32_t c2, uint32_t c3) {
@@ -294,6 +300,26 @@ hipError_t tgp_gibbs(const double* b, const double* y, int n, int D, long long N
   for (double* p : {temp, V, Cm, Ck, M, x, z, W, tnew})
     if (p) (void)hipFreeAsync(p, st);
   return e;
+}
+
+// out = L⁻ᵀz + ysc·M⁻¹(A·y), M = alpha·A·Aᵀ + beta·I = L·Lᵀ (A: p × N column-major, z on the
+// Philox normal stream (c1, c2, c3)): the Gaussian conditional draw of a linear-Gaussian block
+// (GPT_fullw_gibbs w | U, V, 100k_movielensExperiment.jl:1087-1094).  Scratch: M (p²), x, z (p).
+hipError_t gaussian_draw_dense(const double* A, int p, long long N, const double* y, double alpha,
+                               double beta, double ysc, uint64_t seed, uint32_t c1, uint32_t c2,
+                               uint32_t c3, double* M, double* x, double* z, double* out,
+                               int32_t* status, hipStream_t st) {
+  const int T = (p + 15) / 16;
+  hipLaunchKernelGGL(syrk_mfma_kernel, nblk((long long)T * (T + 1) / 2, 4), 256, 0, st, A, p, N,
+                     alpha, beta, M);
+  hipLaunchKernelGGL(gemv_kernel, nblk(p, 256), 256, 0, st, A, p, N, y, ysc, x);
+  hipLaunchKernelGGL(chol_kernel, 1, kTgpNT, 0, st, M, p, status);
+  hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, p, x, 0);
+  hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, p, x, 1);          // mu = M⁻¹(ysc·A·y)
+  hipLaunchKernelGGL(normals_kernel, nblk(p, 256), 256, 0, st, z, p, seed, c1, c2, c3);
+  hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, p, z, 1);          // L⁻ᵀz
+  hipLaunchKernelGGL(gmc_sum_kernel, nblk(p, 256), 256, 0, st, z, x, out, p);
+  return hipGetLastError();
 }
 
 // ============================================================================ GPT_GMC

@@ -5,6 +5,9 @@ BASELINE config 5) on libgptsgld.so.
                        w_init, m, epsw, epsU, a, b, c, burnin, maxepoch, param_seed,
                        ytrainMean, ytrainStd; langevin=False, stiefel=False, avg=False)
                                                              100k_movielensExperiment.jl:409-551
+    GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w,
+                    w_init, burnin, maxepoch, n_samples, param_seed, ytrainMean, ytrainStd;
+                    avg=False, rotated_w=False)              100k_movielensExperiment.jl:1032-1129
     fold(data, i)     the standardised u{i}.base / u{i}.test split of :566-576
 
 Same argument meaning and return tuple as the reference: (w_store, U_store, V_store,
@@ -17,7 +20,7 @@ import numpy as np
 from ._lib import P_D, check, lib
 from . import _lib
 
-__all__ = ["GPT_fullw_sideinfo", "fold"]
+__all__ = ["GPT_fullw_sideinfo", "GPT_fullw_gibbs", "fold"]
 
 
 def _f64(a):
@@ -71,4 +74,28 @@ def GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigm
         print("Get NaN when moving along Geodesic. Try smaller epsU")
     else:
         check(code)
+    return w_store, U_store, V_store, tps, trm, tsm
+
+
+def GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w, w_init,
+                    burnin, maxepoch, n_samples, param_seed, ytrainMean, ytrainStd, avg=False,
+                    rotated_w=False):
+    Rt = _f64(Rating)
+    Rs = _f64(Ratingtest)
+    w0 = _f64(w_init)
+    N, Ntest = Rt.shape[0], Rs.shape[0]
+    n1, n2 = np.shape(UserData)[0], np.shape(MovieData)[0]
+    r = w0.shape[0]
+    w_store = np.zeros((r, r, maxepoch), order="F")
+    U_store = np.zeros((n1, r, maxepoch), order="F")
+    V_store = np.zeros((n2, r, maxepoch), order="F")
+    tps = np.zeros((Ntest, maxepoch), order="F")
+    trm = np.zeros(maxepoch)
+    tsm = np.zeros(maxepoch)
+    check(lib().gpt_cf_fullw_gibbs(
+        _ptr(Rt), N, N, n1, n2, _ptr(Rs), Ntest, Ntest, float(signal_var), float(sigma_u),
+        float(sigma_w), _ptr(w0), r, int(burnin), int(maxepoch), int(n_samples),
+        int(param_seed) & (2 ** 64 - 1), float(ytrainMean), float(ytrainStd), int(bool(avg)),
+        int(bool(rotated_w)), _ptr(w_store), _ptr(U_store), _ptr(V_store), _ptr(tps), _ptr(trm),
+        _ptr(tsm)))
     return w_store, U_store, V_store, tps, trm, tsm

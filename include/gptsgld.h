@@ -224,6 +224,21 @@ int gpt_cf_fullw_sideinfo(const double* Rating, int64_t N, int64_t ldr, const do
                           double* U_store, double* V_store, double* testpred_store,
                           double* trainRMSE, double* testRMSE);
 
+/* GPT_fullw_gibbs(Rating,UserData,MovieData,Ratingtest,signal_var,sigma_u,sigma_w,w_init,burnin,
+ *   maxepoch,n_samples,param_seed;avg,rotated_w)  100k_movielensExperiment.jl:1032-1129: Gibbs
+ * sweeps of the CF model without side information (U: n1 x r, V: n2 x r rows | the rest, then
+ * w | U, V through the N x r^2 Kronecker design).  n1 / n2 are size(UserData,1) / size(MovieData,1);
+ * ytrainMean / ytrainStd are arguments (the reference reads script globals).  Outputs as
+ * gpt_cf_fullw_sideinfo with U_store (n1,r,maxepoch), V_store (n2,r,maxepoch).
+ * GPT_ERR_NOT_SPD on a non positive definite precision (Julia's PosDefException). */
+int gpt_cf_fullw_gibbs(const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2,
+                       const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var,
+                       double sigma_u, double sigma_w, const double* w_init, int64_t r,
+                       int64_t burnin, int64_t maxepoch, int64_t n_samples, uint64_t seed,
+                       double ytrainMean, double ytrainStd, int32_t avg, int32_t rotated_w,
+                       double* w_store, double* U_store, double* V_store, double* testpred_store,
+                       double* trainRMSE, double* testRMSE);
+
 const char* gpt_last_error(void);
 /* LDS bytes one step workgroup needs for this shape (must be <= 163840). */
 int64_t gpt_sgld_lds_bytes(int64_t n, int64_t D, int64_t r, int64_t Q, int64_t m);

@@ -153,3 +153,90 @@ def GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigm
         if testcounter >= 5:
             break
     return w_store, U_store, V_store, testpred_store, trainRMSE, testRMSE
+
+
+def GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w, w_init,
+                    burnin, maxepoch, n_samples, param_seed, ytrainMean, ytrainStd, avg=False,
+                    rotated_w=False):
+    """100k_movielensExperiment.jl:1032-1129 — Gibbs sampling of the tensor CF model without
+    side information: per sweep every user row U_i | V, w, every movie row V_j | U, w (r × r
+    Gaussian conditionals through chol(·,:U)), then w | U, V with the N × r² Kronecker design
+    (kron(V[movie,:], U[user,:]) rows, r² × r² conditional).  Draws (framework contract):
+    Q = qr(randn(r,r)) on (CFG_INIT, 0), U = σ_u·randn(n1, r) on (CFG_INIT, 1), V on (CFG_INIT, 2);
+    sweep g (counted from 0 over the run) draws user i's z on (g, CFG_U, i), movie j's on
+    (g, CFG_V, j) and w's on (g, CFG_W, 0).  ``\`` (a general LU solve in the reference) is taken
+    through the Cholesky factor.  ytrainMean / ytrainStd are arguments (the reference reads the
+    script's globals, :1100); the train prediction is a running average like the test one (the
+    reference re-allocates it uninitialised every epoch, :1098, which only matters when avg).
+    Returns (w_store (r,r,T), U_store (n1,r,T), V_store (n2,r,T), testpred_store, trainRMSE,
+    testRMSE)."""
+    Rating = np.asarray(Rating, dtype=np.float64)
+    Ratingtest = np.asarray(Ratingtest, dtype=np.float64)
+    N, Ntest = len(Rating), len(Ratingtest)
+    n1, n2 = UserData.shape[0], MovieData.shape[0]
+    w0 = np.array(w_init, dtype=np.float64, order="F")
+    r = w0.shape[0]
+    Qm, _ = np.linalg.qr(px.normals(r * r, param_seed, 0, px.CFG_INIT, 0).reshape((r, r), order="F"))
+    U = sigma_u * px.normals(n1 * r, param_seed, 0, px.CFG_INIT, 1).reshape((n1, r), order="F")
+    V = sigma_u * px.normals(n2 * r, param_seed, 0, px.CFG_INIT, 2).reshape((n2, r), order="F")
+    if rotated_w:
+        w = Qm @ w0
+        U = U @ Qm.T
+    else:
+        w = w0.copy()
+    users = Rating[:, 0].astype(np.int64) - 1
+    movies = Rating[:, 1].astype(np.int64) - 1
+    y = Rating[:, 2]
+    w_store = np.zeros((r, r, maxepoch), order="F")
+    U_store = np.zeros((n1, r, maxepoch), order="F")
+    V_store = np.zeros((n2, r, maxepoch), order="F")
+    testpred_store = np.zeros((Ntest, maxepoch), order="F")
+    trainRMSE, testRMSE = np.zeros(maxepoch), np.zeros(maxepoch)
+    trainpred, testpred = np.zeros(N), np.zeros(Ntest)
+    counter = 0
+    sweep = 0
+
+    def draw(prec, rhs, z):
+        L = np.linalg.cholesky(prec)
+        mu = np.linalg.solve(L.T, np.linalg.solve(L, rhs)) / signal_var
+        return np.linalg.solve(L.T, z) + mu
+
+    for epoch in range(1, burnin + maxepoch + 1):
+        for _ in range(n_samples):
+            for i in range(n1):                                                 # :1060-1071
+                sel = users == i
+                if sel.any():
+                    X = V[movies[sel]] @ w.T
+                    prec = X.T @ X / signal_var + np.eye(r) / sigma_u ** 2
+                    U[i] = draw(prec, X.T @ y[sel], px.normals(r, param_seed, sweep, px.CFG_U, i))
+            for j in range(n2):                                                 # :1074-1085
+                sel = movies == j
+                if sel.any():
+                    X = U[users[sel]] @ w
+                    prec = X.T @ X / signal_var + np.eye(r) / sigma_u ** 2
+                    V[j] = draw(prec, X.T @ y[sel], px.normals(r, param_seed, sweep, px.CFG_V, j))
+            K = (V[movies][:, :, None] * U[users][:, None, :]).reshape((N, r * r))   # kron(V, U)
+            prec = K.T @ K / signal_var + np.eye(r * r) / sigma_w ** 2                  # :1092
+            w = draw(prec, K.T @ y, px.normals(r * r, param_seed, sweep, px.CFG_W, 0)).reshape(
+                (r, r), order="F")
+            sweep += 1
+        if epoch > burnin:
+            s = epoch - burnin - 1
+            w_store[:, :, s] = w
+            U_store[:, :, s] = U
+            V_store[:, :, s] = V
+            if not avg:
+                counter = 0
+            ptr = np.einsum("ik,kj,ij->i", U[users], w, V[movies])
+            trainpred = (trainpred * counter + ptr) / (counter + 1)
+            ft = cutoff(trainpred * ytrainStd + ytrainMean)
+            trainRMSE[s] = math.sqrt(np.sum((ytrainStd * y + ytrainMean - ft) ** 2) / N)
+            tu = Ratingtest[:, 0].astype(np.int64) - 1
+            tm = Ratingtest[:, 1].astype(np.int64) - 1
+            pte = np.einsum("ik,kj,ij->i", U[tu], w, V[tm])
+            testpred = (testpred * counter + pte) / (counter + 1)
+            fs = cutoff(testpred * ytrainStd + ytrainMean)
+            testpred_store[:, s] = fs
+            testRMSE[s] = math.sqrt(np.sum((ytrainStd * Ratingtest[:, 2] + ytrainMean - fs) ** 2) / Ntest)
+            counter += 1
+    return w_store, U_store, V_store, testpred_store, trainRMSE, testRMSE

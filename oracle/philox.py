@@ -42,6 +42,8 @@ TGP_U_INIT, TGP_I, TGP_W_NOISE, TGP_U_NOISE = 11, 12, 13, 14
 GMC_P, GMC_MOM, GMC_U = 15, 16, 17
 # MovieLens tensor CF (100k_movielensExperiment.jl:409-551): U/V init, w noise, U/V noise
 CF_UV_INIT, CF_W_NOISE, CF_UV_NOISE = 18, 19, 20
+# GPT_fullw_gibbs (100k_movielensExperiment.jl:1032-1129): init (QR draw, U, V), per-sweep draws
+CFG_INIT, CFG_U, CFG_V, CFG_W = 21, 22, 23, 24
 
 
 def philox4x32(c0, c1, c2, c3, seed):

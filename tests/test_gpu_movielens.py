@@ -68,3 +68,29 @@ def test_fullw_sideinfo_live_config_full_fold():
     assert rel(got[0], want[0]) < 1e-8 and rel(got[1], want[1]) < 1e-8 and rel(got[2], want[2]) < 1e-8
     assert abs(got[5][0] - want[5][0]) <= 1e-9 * want[5][0]
     assert 0.8 < got[5][0] < 1.3                      # test RMSE on the 1..5 rating scale
+
+
+GIBBS_CASES = {
+    # name: (ntrain, ntest, r, burnin, maxepoch, n_samples, avg, rotated_w)
+    "plain": (3000, 1000, 4, 0, 2, 1, False, False),
+    "avg_rotated": (2500, 700, 3, 1, 2, 2, True, True),
+    "r15_fold": (6000, 1500, 15, 0, 1, 1, False, False),      # r = 15 of :723 (r² = 225 design)
+}
+
+
+@pytest.mark.parametrize("name", list(GIBBS_CASES))
+def test_fullw_gibbs_matches_oracle(name):
+    """GPT_fullw_gibbs (100k_movielensExperiment.jl:1032-1129): per-user / per-movie r × r
+    conditionals in one wave each, w | U, V through the fp64-MFMA SYRK of the Kronecker design."""
+    from gpt_amd import movielens
+    ntr, nte, r, bi, ep, ns, avg, rot = GIBBS_CASES[name]
+    tr, te, ud, md, mu, sd = problem(ntr, nte)
+    w0 = np.random.default_rng(9).standard_normal((r, r))
+    args = (tr, ud, md, te, 0.8, 0.5, 1.0, w0, bi, ep, ns, 17, mu, sd)
+    got = movielens.GPT_fullw_gibbs(*args, avg=avg, rotated_w=rot)
+    want = M.GPT_fullw_gibbs(*args, avg=avg, rotated_w=rot)
+    for g, w_ in zip(got[:3], want[:3]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    assert np.abs(got[3] - want[3]).max() < 1e-8
+    assert np.all(np.abs(got[4] - want[4]) <= 1e-9 * want[4])
+    assert np.all(np.abs(got[5] - want[5]) <= 1e-9 * want[5])
