@@ -1,0 +1,39 @@
+"""Wall-clock of the MovieLens-100k CF samplers on the GPU (config 5): the live GPT_fullw_sideinfo
+run of 100k_movielensExperiment.jl:723-730 (fold 1, r = 15, m = 100) and one GPT_fullw_gibbs
+sweep, printed as one JSON line.  Usage: python scripts/time_movielens.py [--epochs E]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=5)
+    args = ap.parse_args()
+    from gpt_amd import movielens
+    d = np.load(os.path.join(ROOT, "tests", "golden", "ml100k.npz"))
+    tr, te, ud, md, mu, sd = movielens.fold(d, 1)
+    w0 = np.random.default_rng(17).standard_normal((15, 15))
+    movielens.GPT_fullw_sideinfo(tr, ud, md, te, 0.8, 0.1, 1.0, w0, 100, 1e-4, 1e-6, 0.5, 0.25,
+                                 0.5, 0, 1, 17, mu, sd)                        # warm-up / load
+    t = time.perf_counter()
+    out = movielens.GPT_fullw_sideinfo(tr, ud, md, te, 0.8, 0.1, 1.0, w0, 100, 1e-4, 1e-6, 0.5,
+                                       0.25, 0.5, 0, args.epochs, 17, mu, sd)
+    ts = (time.perf_counter() - t) / args.epochs
+    t = time.perf_counter()
+    g = movielens.GPT_fullw_gibbs(tr, ud, md, te, 0.8, 0.5, 1.0, w0, 0, 2, 1, 17, mu, sd)
+    tg = (time.perf_counter() - t) / 2
+    print(json.dumps({"workload": "ml-100k fold 1, r=15", "sideinfo_sgd_s_per_epoch": ts,
+                      "sideinfo_steps_per_s": 800 / ts, "sideinfo_testRMSE": list(out[5]),
+                      "gibbs_s_per_sweep": tg, "gibbs_testRMSE": list(g[5])}))
+
+
+if __name__ == "__main__":
+    main()
