@@ -104,7 +104,8 @@ def main():
     ap.add_argument("--kernel-steps", type=int, default=100, help="steps of the event-timed pass")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--single-chain", action="store_true", help="also time C=1 latency")
+    ap.add_argument("--no-single-chain", dest="single_chain", action="store_false",
+                    help="skip the C=1 latency pass (one chain on one CU)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 

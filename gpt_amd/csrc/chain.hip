@@ -345,7 +345,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       }
     }
 #if CHAIN_STAGE_AT == 3 && !CHAIN_DBUF
-    if (g0 + G < Bt) stage(g0 + G, ln, pw);
+    if (!CHAIN_EXP_NOSTAGE && g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
     lds_barrier();
 #if CHAIN_STAGE_AT == 1 && !CHAIN_DBUF

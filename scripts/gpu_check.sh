@@ -10,6 +10,6 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 420 python -m pytest tests -m gpu -q -rf > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -25 gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 1000 --warmup 200 --single-chain} > gpurun_out/bench.log 2>&1
+timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 1000 --warmup 200} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
 exit $rc

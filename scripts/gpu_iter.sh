@@ -10,6 +10,6 @@ timeout -k 10 120 python scripts/phase_stamps.py --engine chain --chains 1 --ste
 rc=$?; echo "stamps1 rc=$rc"; cat gpurun_out/stamps_c1.log | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python scripts/phase_stamps.py --engine chain --chains 256 --steps 10 > gpurun_out/stamps_c256.log 2>&1
 rc=$?; echo "stamps256 rc=$rc"; cat gpurun_out/stamps_c256.log | grep -v amdgpu.ids; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python bench.py --engine chain --steps 1000 --warmup 100 --no-cpu-baseline --single-chain ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+timeout -k 10 200 python bench.py --engine chain --steps 1000 --warmup 100 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('value %.0f ms/step %.4f kern_us %.1f frac %.3f single %.0f rmse %.4f' % (d['value'], d['ms_per_step'], d['roofline']['kernel_us'], d['roofline']['frac'], d['single_chain_steps_per_s'] or 0, d['test_rmse']))"
 exit $rc
