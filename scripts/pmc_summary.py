@@ -19,13 +19,28 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_dispatch(path, counter, match):
+def per_dispatch(path, counter, match, grid=None):
     vals = []
     with open(path) as f:
         for row in csv.DictReader(f):
             if row["Counter_Name"] == counter and match in row["Kernel_Name"]:
-                vals.append(float(row["Counter_Value"]))
+                if grid is None or int(row["Grid_Size"]) == grid:
+                    vals.append(float(row["Counter_Value"]))
     return vals
+
+
+def timed_launches(path, match):
+    """(grid size, durations in us) of the bench's timed launches: the largest grid of the
+    kernel (bench.py also runs a one-chain latency pass of the same kernel)."""
+    by = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if match in row["Kernel_Name"]:
+                g = int(row["Grid_Size_X"]) * int(row["Grid_Size_Y"]) * int(row["Grid_Size_Z"])
+                by.setdefault(g, []).append(
+                    (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1000.0)
+    g = max(by)
+    return g, by[g]
 
 
 def main():
@@ -48,15 +63,20 @@ def main():
                 break
     if avg_ns is None:
         sys.exit("kernel %s not in %s" % (args.kernel, stats))
+    grid, durs = timed_launches(os.path.join(args.outdir, "stats", "run_kernel_trace.csv"),
+                                args.kernel)
     fetch = per_dispatch(os.path.join(args.outdir, "fetch", "run_counter_collection.csv"),
-                         "FETCH_SIZE", args.kernel)
+                         "FETCH_SIZE", args.kernel, grid)
     write = per_dispatch(os.path.join(args.outdir, "write", "run_counter_collection.csv"),
-                         "WRITE_SIZE", args.kernel)
+                         "WRITE_SIZE", args.kernel, grid)
     fm, wm = statistics.median(fetch), statistics.median(write)
     entry = {
         "kernel": name.split("(")[0].replace("void ", ""),
-        "avg_duration_us": avg_ns / 1000.0,
+        "avg_duration_us_all_launches": avg_ns / 1000.0,
         "calls": calls,
+        "timed_grid_threads": grid,
+        "avg_duration_us": statistics.mean(durs),
+        "timed_launches": len(durs),
         "FETCH_SIZE_KB_median": fm,
         "WRITE_SIZE_KB_median": wm,
         "launches": len(fetch),
