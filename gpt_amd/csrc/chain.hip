@@ -332,16 +332,16 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
     double sacc[G];
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
-      sacc[gg] = 0.0;
+      sacc[gg] = bscr[(gg * R + rl) * kChainRunS + rs];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) sacc[gg] += bscr[(gg * R + rl) * kChainRunS + rs + 8 * i];
+      for (int i = 1; i < 8; ++i) sacc[gg] += bscr[(gg * R + rl) * kChainRunS + rs + 8 * i];
     }
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
       const double sv = group8_sum(sacc[gg]);
       if (rs == 0 && (ln >> 3) < R) {
         tsl[(k * R + rl) * G + gg] = sv;
-        tsl[DRG + G + (k * R + rl) * G + gg] = 1.0 / sv;
+        tsl[DRG + G + (k * R + rl) * G + gg] = rcp_nr(sv);
       }
     }
 #if CHAIN_STAGE_AT == 3 && !CHAIN_DBUF
@@ -385,9 +385,9 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
     double res[G];
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
-      double f = 0.0;
+      double f = fp_l[gg * kChainQPL];
 #pragma unroll
-      for (int c = 0; c < kChainQPL; ++c) f += fp_l[gg * kChainQPL + c];   // unused chunks are 0
+      for (int c = 1; c < kChainQPL; ++c) f += fp_l[gg * kChainQPL + c];   // unused chunks are 0
       res[gg] = (g0 + gg < Bt) ? y_l[g0 + gg] - f : 0.0;
     }
 #pragma unroll
@@ -396,13 +396,14 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
       // :248-273): lane 8l+s sums members s, s+8, .., the 8-lane group finishes with DPP; lane
       // 8l then holds A[l]
       const double* wr = wVr + gg * kChainQS;
-      double a = 0.0;
+      double a = wr[gq[0] & 0xffff];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a += wr[(gq[i >> 1] >> (16 * (i & 1))) & 0xffff];
-      a = group8_sum(a) * tsl[DRG + G + (k * R + rl) * G + gg];
+      for (int i = 1; i < 8; ++i) a += wr[(gq[i >> 1] >> (16 * (i & 1))) & 0xffff];
+      // A·res formed on every lane before the broadcast (same two products as A then ·res)
+      a = (group8_sum(a) * tsl[DRG + G + (k * R + rl) * G + gg]) * res[gg];
       double cc[R];
 #pragma unroll
-      for (int l = 0; l < R; ++l) cc[l] = readlane_d(a, 8 * l) * res[gg];
+      for (int l = 0; l < R; ++l) cc[l] = readlane_d(a, 8 * l);
 #pragma unroll
       for (int jj = 0; jj < J; ++jj) {
 #if CHAIN_DBUF

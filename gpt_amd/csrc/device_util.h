@@ -27,8 +27,10 @@ __device__ __forceinline__ void wave_sync() {
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  // every control used here is a full permutation within a row, so no lane keeps its old
+  // value: mov_dpp (old = undef) needs no zero-initialised destination
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 template <int OFF>
@@ -78,6 +80,16 @@ __device__ __forceinline__ double group8_sum(double v) {
   v += dpp_partner<1>(v);
   v += dpp_partner<2>(v);
   return v + dpp_partner<4>(v);     // row_half_mirror pairs the two quads of the group
+}
+
+// 1/x from the hardware reciprocal plus two Newton steps (within 1 ulp; 5 VALU ops instead of
+// the ~10 of an IEEE division).
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {

@@ -145,6 +145,23 @@ def test_sampler_trajectory_matches_oracle(name, engine):
                 assert np.abs(Uk.T @ Uk - np.eye(r)).max() < 1e-10
 
 
+@pytest.mark.parametrize("name", [c for c, e in ENGINE_CASES if e == "chain"])
+def test_chain_trajectory_without_diagnostics(name):
+    """Without per-step gradient norms the chain engine folds the U noise into the gradient
+    accumulator inside the batch loop (chain.hip, noise_block): same samples as the oracle."""
+    n, D, N, r, Q, m, burnin, maxepoch, se, lang, stf = CASES[name]
+    p = make_problem(n, D, N, r, Q, seed=11)
+    epsw, epsU, sv, seed = 1e-4, 1e-6, 0.05, 23
+    ws, Us = G().GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
+                               maxepoch, seed, langevin=lang, stiefel=stf, store_every=se,
+                               engine="chain")
+    wo, Uo, info = R.GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
+                                   maxepoch, seed, langevin=lang, stiefel=stf, store_every=se)
+    assert info["status"] == 0
+    assert rel(ws, wo) < 1e-8, rel(ws, wo)
+    assert rel(Us, Uo) < 1e-8, rel(Us, Uo)
+
+
 RMS_CASES = {
     # name: (n, D, N, r, Q, m, burnin, maxepoch, epsilon)
     "small": (16, 3, 40, 2, 6, 8, 1, 2, 1e-5),
