@@ -46,43 +46,38 @@ constexpr int kChainRunS = 72;    // reduction scratch stride (doubles): 8-lane 
                                   // l, l+1.. hit disjoint LDS bank ranges (72·2 dwords ≡ 16 banks)
 constexpr int kChainQS = 264;     // w·V row stride; slot kChainQP of a row is a constant 0
 
-struct ChainLayout {
-  int NCH, NT;                    // q chunks of 64, tasks = NCH·G
-  int TS;                         // doubles per temp slot: temp | ones(G) | 1/temp | ones(G)
-  size_t o_IT, o_w, o_idx, o_y, o_temp, o_fp, o_gwp, o_misc, o_un, bytes;
-  size_t L_dbl, x_dbl;            // union tenants (doubles): w·V rows + reduction scratch | per-wave scratch
-};
+constexpr int kChainMMax = 256;   // largest minibatch the engine takes
 
 // Per-wave scratch after the batch: S0 = max(expm<2r> scratch, noise slots) | E[:,1:r] | grams.
-GPT_HD size_t chain_scratch_dbl(int r) {
-  const size_t s0a = 7 * 4 * (size_t)r * r, s0b = 64 * (size_t)(r + (r & 1));
-  return (s0a > s0b ? s0a : s0b) + 2 * (size_t)r * r + 3 * (size_t)r * r + r;
+GPT_HD constexpr int chain_scratch_dbl(int r) {
+  const int s0a = 7 * 4 * r * r, s0b = 64 * (r + (r & 1));
+  return (s0a > s0b ? s0a : s0b) + 2 * r * r + 3 * r * r + r;
 }
+GPT_HD constexpr int al16c(int x) { return (x + 15) & ~15; }
 
-GPT_HD ChainLayout chain_layout(int n, int D, int r, int Q, int m, int G) {
-  (void)n;
-  ChainLayout L;
-  L.NCH = (Q + 63) / 64;
-  L.NT = L.NCH * G;
-  L.TS = 2 * (D * r * G + G);
-  size_t o = 0;
-  // index tables for all kChainDMax dimensions (rows k >= D point at the ones / trash slots)
-  L.o_IT = o;   o = al16(o + 4 * (size_t)Q * kChainDMax);
-  L.o_w = o;    o = al16(o + 8 * (size_t)Q);
-  L.o_idx = o;  o = al16(o + 4 * (size_t)m);
-  L.o_y = o;    o = al16(o + 8 * (size_t)m);
-  L.o_temp = o; o = al16(o + 8 * 2 * (size_t)L.TS);           // 2 slots
-  L.o_fp = o;   o = al16(o + 8 * (size_t)kChainQPL * G);
-  L.o_gwp = o;  o = al16(o + 8 * (size_t)L.NT * 64);
-  L.o_misc = o; o = al16(o + 8 * 16);
-  L.o_un = o;
-  // batch-loop tenants: w·V rows [row][q] (stride kChainQS) | per-wave reduction scratch
-  L.L_dbl = (size_t)G * kChainQS + (size_t)D * G * r * kChainRunS;
-  L.x_dbl = chain_scratch_dbl(r);
-  const size_t un = 8 * (L.L_dbl > L.x_dbl * D ? L.L_dbl : L.x_dbl * D);
-  L.bytes = al16(o + un);
-  return L;
-}
+// LDS carve of chain_kernel<R, J, G>, fixed at compile time: every table is sized for the
+// engine's maxima (kChainDMax dimensions, Q <= kChainQP, m <= kChainMMax), so every LDS address
+// is a constant and none of them occupies a scalar register (the kernel sits at the SGPR limit).
+template <int R, int G>
+struct ChainLds {
+  static constexpr int DRG = kChainDMax * R * G;          // temp entries of a slot
+  static constexpr int TS = 2 * (DRG + G);                // temp | ones(G) | 1/temp | ones(G)
+  static constexpr int NTMAX = kChainQPL * G;             // V tasks at Q = kChainQP
+  static constexpr int o_IT = 0;                                         // int[kChainDMax][Q]
+  static constexpr int o_w = al16c(o_IT + 4 * kChainQP * kChainDMax);    // double[Q]
+  static constexpr int o_idx = al16c(o_w + 8 * kChainQP);                // int[m]
+  static constexpr int o_y = al16c(o_idx + 4 * kChainMMax);              // double[m]
+  static constexpr int o_temp = al16c(o_y + 8 * kChainMMax);             // 2 slots
+  static constexpr int o_fp = al16c(o_temp + 8 * 2 * TS);
+  static constexpr int o_gwp = al16c(o_fp + 8 * kChainQPL * G);
+  static constexpr int o_misc = al16c(o_gwp + 8 * NTMAX * 64);
+  static constexpr int o_un = al16c(o_misc + 8 * 16);
+  // union: w·V rows [row][q] (stride kChainQS) + per-wave reduction scratch (batch loop) |
+  // per-wave post-batch scratch
+  static constexpr int L_dbl = G * kChainQS + kChainDMax * G * R * kChainRunS;
+  static constexpr int x_dbl = chain_scratch_dbl(R);
+  static constexpr int bytes = al16c(o_un + 8 * (L_dbl > x_dbl * kChainDMax ? L_dbl : x_dbl * kChainDMax));
+};
 
 // Diagnostic phase stamps (gpt_sgld_session_stamps only): s_memtime of wave 0 at phase ends.
 #define CSTAMP(slot)                                                                        \
@@ -139,21 +134,22 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   const ChainDesc* Cp = chains + blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, k = uni(tid >> 6);
   const int n = P.n, D = P.D, Q = P.Q, m = P.m, NTH = 64 * D;
-  const ChainLayout L = chain_layout(n, D, R, Q, m, G);
-  int* IT_l = (int*)(smem + L.o_IT);
-  double* w_l = (double*)(smem + L.o_w);
-  int* idx_l = (int*)(smem + L.o_idx);
-  double* y_l = (double*)(smem + L.o_y);
-  double* temp_l = (double*)(smem + L.o_temp);
-  double* fp_l = (double*)(smem + L.o_fp);
-  double* gwp_l = (double*)(smem + L.o_gwp);
-  double* misc = (double*)(smem + L.o_misc);
+  using L = ChainLds<R, G>;
+  const int NCH = (Q + 63) / 64, NT = NCH * G;                  // q chunks of 64, V tasks
+  int* IT_l = (int*)(smem + L::o_IT);
+  double* w_l = (double*)(smem + L::o_w);
+  int* idx_l = (int*)(smem + L::o_idx);
+  double* y_l = (double*)(smem + L::o_y);
+  double* temp_l = (double*)(smem + L::o_temp);
+  double* fp_l = (double*)(smem + L::o_fp);
+  double* gwp_l = (double*)(smem + L::o_gwp);
+  double* misc = (double*)(smem + L::o_misc);
   int* flag = (int*)(misc + 8);
-  double* wVr = (double*)(smem + L.o_un);                       // w_q·V_q per batch row
-  double* X = (double*)(smem + L.o_un) + (size_t)k * L.x_dbl;   // this wave's scratch
+  double* wVr = (double*)(smem + L::o_un);                      // w_q·V_q per batch row
+  double* X = (double*)(smem + L::o_un) + k * L::x_dbl;         // this wave's scratch
   double* xi_l = X;                                             // noise slots (before expm)
   double* pw0 = pbuf + k * (kChainBufs * G * 64 * J);           // this wave's staged rows
-  double* bscr = wVr + (size_t)G * kChainQS + (size_t)k * G * R * kChainRunS;   // per row
+  double* bscr = wVr + G * kChainQS + k * G * R * kChainRunS;   // per row
 
   const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
@@ -211,7 +207,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   }
 
   // ---- prologue: index tables, w, batch rows, and U^(k) into registers
-  const int DRG = D * R * G;
+  constexpr int DRG = L::DRG;           // temp entries of all kChainDMax dimensions
   {
     // IT_l[kk·Q+q]: temp index (kk·R + I[q,kk])·G of the core entry (+gg at use); rows kk >= D
     // point at the ones slot.
@@ -221,8 +217,8 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
     }
     for (int o = tid; o < G; o += NTH) wVr[o * kChainQS + kChainQP] = 0.0;   // gather zero slots
     for (int o = tid; o < 2 * G; o += NTH) {                     // ones slots of both temp slots
-      temp_l[o / G * L.TS + DRG + o % G] = 1.0;
-      temp_l[o / G * L.TS + 2 * DRG + G + o % G] = 1.0;
+      temp_l[o / G * L::TS + DRG + o % G] = 1.0;
+      temp_l[o / G * L::TS + 2 * DRG + G + o % G] = 1.0;
     }
     for (int o = tid; o < kChainQPL * G; o += NTH) fp_l[o] = 0.0;
   }
@@ -270,7 +266,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #pragma unroll
   for (int x = 0; x < TPW; ++x) {
     const int task = k + D * x;
-    const int c = task < L.NT ? task % L.NCH : 0;
+    const int c = task < NT ? task % NCH : 0;
     const int qq = min(64 * c + lane, Q - 1);
 #pragma unroll
     for (int h = 0; h < kChainDMax / 4; ++h) {
@@ -314,7 +310,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #endif
     // (b) temp[k,l,row] and 1/temp for the G rows: R partial dots per lane, reduced through this
     // wave's LDS scratch by 8-lane groups (lane 8l+s sums 8 partials of output l, DPP finishes)
-    double* tsl = temp_l + slot * L.TS;
+    double* tsl = temp_l + slot * L::TS;
     const int rl = min(ln >> 3, R - 1), rs = ln & 7;
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
@@ -355,8 +351,8 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #pragma unroll
     for (int x = 0; x < TPW; ++x) {
       const int task = k + D * x;
-      if (task >= L.NT || CHAIN_EXP_NOV) break;
-      const int gg = task / L.NCH, c = task - gg * L.NCH;
+      if (task >= NT || CHAIN_EXP_NOV) break;
+      const int gg = task / NCH, c = task - gg * NCH;
       const int q = 64 * c + ln;
       const bool ok = q < Q;
       const int qq = ok ? q : 0;
@@ -418,8 +414,8 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #pragma unroll
     for (int x = 0; x < TPW; ++x) {
       const int task = k + D * x;
-      if (task >= L.NT) break;
-      const int gg = task / L.NCH;
+      if (task >= NT) break;
+      const int gg = task / NCH;
       double rr = res[0];
 #pragma unroll
       for (int g2 = 1; g2 < G; ++g2) if (gg == g2) rr = res[g2];
@@ -438,7 +434,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
 #pragma unroll
   for (int x = 0; x < TPW; ++x) {
     const int task = k + D * x;
-    if (task >= L.NT) break;
+    if (task >= NT) break;
     gwp_l[task * 64 + lane] = gw[x];
   }
   __syncthreads();
@@ -450,7 +446,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
     for (int q = tid; q < Q; q += NTH) {
       const int c = q >> 6, ln = q & 63;
       double g = 0.0;
-      for (int gg = 0; gg < G; ++gg) g += gwp_l[(gg * L.NCH + c) * 64 + ln];
+      for (int gg = 0; gg < G; ++gg) g += gwp_l[(gg * NCH + c) * 64 + ln];
       const double wq = w_l[q];
       const double gradw = cN * g / C.signal_var - wq * inv_sw2;
       double step = C.epsw * gradw / 2;
@@ -672,7 +668,15 @@ static size_t chain_static_lds(int J) { return 8 * (size_t)kChainBufs * kChainDM
 static int chain_J(int n) { return n <= 64 ? 1 : (n <= 128 ? 2 : (n <= 256 ? 4 : (n <= 512 ? 8 : 0))); }
 
 size_t chain_lds_bytes(int n, int D, int r, int Q, int m) {
-  return chain_layout(n, D, r, Q, m, kChainG).bytes;
+  (void)n; (void)D; (void)Q; (void)m;
+  switch (r) {
+    case 1: return ChainLds<1, kChainG>::bytes;
+    case 2: return ChainLds<2, kChainG>::bytes;
+    case 3: return ChainLds<3, kChainG>::bytes;
+    case 4: return ChainLds<4, kChainG>::bytes;
+    case 5: return ChainLds<5, kChainG>::bytes;
+    default: return (size_t)1 << 30;
+  }
 }
 
 bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stiefel, int max_run) {
@@ -680,10 +684,10 @@ bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stie
   if (!langevin || !stiefel) return false;   // SGD / Euclidean variants run on the grid engine
   if (D < 1 || D > kChainDMax || r < 1 || r > 5 || chain_J(n) == 0) return false;
   if (chain_J(n) >= 2 && (n & 1)) return false;   // 16-B row staging needs 16-B aligned rows
-  const ChainLayout L = chain_layout(n, D, r, Q, m, kChainG);
-  if (Q > kChainQP) return false;
-  if (L.NT > (chain_J(n) >= 8 ? 1 : kChainTasks) * D) return false;
-  return L.bytes + chain_static_lds(chain_J(n)) <= 160 * 1024;
+  if (Q > kChainQP || m > kChainMMax) return false;   // the fixed LDS carve's maxima
+  const int NT = (Q + 63) / 64 * kChainG;
+  if (NT > (chain_J(n) >= 8 ? 1 : kChainTasks) * D) return false;
+  return chain_lds_bytes(n, D, r, Q, m) + chain_static_lds(chain_J(n)) <= 160 * 1024;
 }
 
 hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchains,
