@@ -158,7 +158,7 @@ def GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigm
 def GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w, w_init,
                     burnin, maxepoch, n_samples, param_seed, ytrainMean, ytrainStd, avg=False,
                     rotated_w=False):
-    """100k_movielensExperiment.jl:1032-1129 — Gibbs sampling of the tensor CF model without
+    r"""100k_movielensExperiment.jl:1032-1129 — Gibbs sampling of the tensor CF model without
     side information: per sweep every user row U_i | V, w, every movie row V_j | U, w (r × r
     Gaussian conditionals through chol(·,:U)), then w | U, V with the N × r² Kronecker design
     (kron(V[movie,:], U[user,:]) rows, r² × r² conditional).  Draws (framework contract):
