@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_MFMA_PEAK_TFS = 78.6     # MI355X dense FP64 matrix peak (AMD spec; v_mfma_f64_16x16x4f64)
 FP64_PEAK_TFLOPS = 78.6        # MI355X fp64 vector/matrix peak (spec)
 
 
@@ -188,16 +189,25 @@ def main():
         except Exception:
             traffic = None
 
-    # test prediction with each chain's final state, ensemble mean over chains and ranks
+    # posterior predictive over every chain's final state as ONE stacked-sample prediction
+    # (fp64-MFMA phidotU GEMM with M = S·r, N = Ntest, K = n per dimension, then the V-phase)
     I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
-    npred = min(C, 8)
-    fsum = torch.zeros(Nte, dtype=torch.float64, device=dev)
-    fh = torch.empty(Nte, dtype=torch.float64, device=dev)
-    for c in range(npred):
-        wp, Up, _, _, _ = sess.device_state(c)
-        pred_device(wp, Up, I0, phi_te, n, D, Nte, r, Q, 1, fh)
-        fsum += fh
+    npred = C
+    w_all = torch.empty((npred, Q), dtype=torch.float64, device=dev)
+    U_all = torch.empty((npred, n * r * D), dtype=torch.float64, device=dev)
+    sess.gather_state(0, npred, w_all, U_all)
+    sess.sync()
+    fh = torch.empty((npred, Nte), dtype=torch.float64, device=dev)
+    pred_device(w_all.data_ptr(), U_all.data_ptr(), I0, phi_te, n, D, Nte, r, Q, npred, fh)
     torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    pred_device(w_all.data_ptr(), U_all.data_ptr(), I0, phi_te, n, D, Nte, r, Q, npred, fh)
+    ev1.record()
+    torch.cuda.synchronize()
+    pred_ms = ev0.elapsed_time(ev1)
+    pred_flop = 2.0 * npred * r * n * D * Nte             # the GEMM (dominant); V-phase excluded
+    fsum = fh.sum(dim=0)
     from gpt_amd.ensemble import combine_predictive_mean, rmse as ens_rmse
     ta = time.perf_counter()
     fmean = combine_predictive_mean(fsum, npred)     # RCCL all-reduce across ranks (config 4)
@@ -249,6 +259,12 @@ def main():
             "test_rmse_note": "ensemble of %d chains x %d ranks after %d steps/chain (%.1f epochs)"
                               % (npred, world, args.warmup + args.steps, (args.warmup + args.steps) / nb),
             "allreduce_ms": allreduce_ms,
+            "pred": {"samples": npred, "Ntest": Nte, "ms": pred_ms, "gemm_flop": pred_flop,
+                     "achieved_tflops": pred_flop / (pred_ms * 1e-3) / 1e12,
+                     "peak_tflops": FP64_MFMA_PEAK_TFS,
+                     "frac": pred_flop / (pred_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS,
+                     "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + pred_vphase_kernel",
+                     "note": "whole stacked-sample call timed with events (GEMM + V-phase)"},
             "single_chain_steps_per_s": single,
         }
         print(json.dumps(out))

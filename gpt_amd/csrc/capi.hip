@@ -604,6 +604,21 @@ extern "C" int gpt_sgld_session_state(gpt_sgld_session* s, int32_t chain, double
   return GPT_OK;
 }
 
+extern "C" int gpt_sgld_session_gather_state(gpt_sgld_session* s, int32_t first, int32_t count,
+                                             double* w_dev_out, double* U_dev_out) {
+  if (!s || first < 0 || count < 0 || first + count > s->nchains || (count && (!w_dev_out || !U_dev_out))) {
+    set_error("bad chain range"); return GPT_ERR_BAD_DIMS;
+  }
+  const size_t Q = (size_t)s->P.Q, nrD = (size_t)s->P.n * s->P.r * s->P.D;
+  for (int32_t c = 0; c < count; ++c) {
+    const ChainDesc& C = s->chains_h[first + c];
+    HIPCHK(hipMemcpyAsync(w_dev_out + c * Q, C.w + (size_t)(s->steps_done & 1) * Q, 8 * Q,
+                          hipMemcpyDeviceToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(U_dev_out + c * nrD, C.U, 8 * nrD, hipMemcpyDeviceToDevice, s->stream));
+  }
+  return GPT_OK;
+}
+
 extern "C" int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double* w_store,
                                       double* U_store, double* diag, int32_t* status) {
   if (!s || chain < 0 || chain >= s->nchains) { set_error("bad chain"); return GPT_ERR_BAD_DIMS; }

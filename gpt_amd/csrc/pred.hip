@@ -2,6 +2,10 @@
 // kin40kExperiment.jl:78-87).
 #include "device_util.h"
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 namespace gpt {
 
 // fhat[s*Ntest + i] = pred(w_s, U_s, I, phitest)[i] for a 64-column tile × one sample.
@@ -190,7 +194,287 @@ __global__ __launch_bounds__(kNT) void mean_sse_kernel(const double* __restrict_
 
 #define GPT_RANKS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(15) X(16) X(20)
 
-hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, const double* phitest,
+// ---- stacked-sample prediction on the fp64 matrix cores (GPT_SGLD.jl:233-243 over S samples)
+//
+// phidotU of S samples at once is one GEMM per dimension k:
+//   T[(s·D + k)·R + l][i] = Σ_j U_s[j, l, k] · phi[j, k, i]     (M = S·R, N = Ntest, K = n)
+// run on v_mfma_f64_16x16x4f64, then the V-phase (computeV / computefhat) per (sample, 64-row tile)
+// reads its R·D temp rows.  Both operands are K(j)-contiguous; lane λ feeds the K pair
+// j0 + 2(λ>>4) + {0,1} of row/column λ&15 as one 16-B load and the two halves go to two MFMAs
+// (any K order common to A and B is the same sum).  A workgroup = 4 waves = a 64(c) × 64(i)
+// tile, each wave 2 × 2 MFMA tiles.  Workgroups are numbered so that the c-tiles of one
+// (i-tile, k) land on the same XCD (dispatch is round-robin over the 8 XCDs): phi[:, k, tile] is
+// then fetched into one L2 and reused there by every c-tile.
+typedef double pd4 __attribute__((ext_vector_type(4)));
+typedef double pd2 __attribute__((ext_vector_type(2)));
+constexpr int kXcds = 8;
+
+template <bool V2>
+__global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __restrict__ U,
+                                                             const double* __restrict__ phi,
+                                                             int n, int D, int R,
+                                                             long long Ntest, int S,
+                                                             double* __restrict__ T) {
+  const int SR = S * R;
+  const int nct = (SR + 63) / 64;
+  const long long nit = (Ntest + 63) / 64;
+  const long long total = (long long)nct * nit * D;
+  const long long per = ((long long)gridDim.x) / kXcds;
+  const long long logical = (long long)(blockIdx.x % kXcds) * per + blockIdx.x / kXcds;
+  if (logical >= total) return;
+  const int ct = (int)(logical % nct);
+  const long long rest = logical / nct;
+  const long long it = rest % nit;
+  const int k = (int)(rest / nit);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, kl = lane >> 4;
+  const int cw = ct * 64 + (wv & 1) * 32;
+  const long long iw = it * 64 + (wv >> 1) * 32;
+  const __attribute__((address_space(1))) double* pa[2];
+  const __attribute__((address_space(1))) double* pb[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int c = cw + 16 * t + (lane & 15);
+    const int cc = c < SR ? c : 0, sm = cc / R, l = cc - sm * R;
+    pa[t] = gptr(U + (size_t)sm * n * R * D + (size_t)n * (l + R * k));
+    const long long i = iw + 16 * t + (lane & 15);
+    pb[t] = gptr(phi + (size_t)n * (k + (size_t)D * (i < Ntest ? i : 0)));
+  }
+  pd4 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[t][u] = pd4{0.0, 0.0, 0.0, 0.0};
+  // Branch- and select-free operand loads in the K loop (address clamped in-row): lanes of
+  // columns c >= S·R or rows i >= Ntest read row 0 and only feed outputs that are never stored,
+  // so the loaded values go straight into the MFMAs and the loads of one step stay in flight
+  // across the other step's MFMAs.  Only the K tail (j >= n) is zeroed, after the loop.
+  auto ld = [&](const __attribute__((address_space(1))) double* p, int j, double& x0, double& x1) {
+    if constexpr (V2) {              // n even: j even, rows 16-B aligned
+      const pd2 v = *(const __attribute__((address_space(1))) pd2*)(p + min(j, n - 2));
+      x0 = v[0]; x1 = v[1];
+    } else {
+      x0 = p[min(j, n - 1)];
+      x1 = p[min(j + 1, n - 1)];
+    }
+  };
+  struct Ops { double a0[2], a1[2], b0[2], b1[2]; };
+  auto load = [&](int j, Ops& o) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      ld(pa[t], j, o.a0[t], o.a1[t]);
+      ld(pb[t], j, o.b0[t], o.b1[t]);
+    }
+  };
+  auto ktail = [&](int j, Ops& o) {    // zero the A halves past n (one operand suffices)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      o.a0[t] = j < n ? o.a0[t] : 0.0;
+      o.a1[t] = j + 1 < n ? o.a1[t] : 0.0;
+    }
+  };
+  // the four independent accumulators with the even K half, then with the odd one (no
+  // back-to-back MFMA on one accumulator)
+  auto mma = [&](const Ops& o) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.a0[t], o.b0[u], acc[t][u], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.a1[t], o.b1[u], acc[t][u], 0, 0, 0);
+  };
+  // two K steps of 8 per iteration over the full 16-blocks, ping-ponging two operand sets: one
+  // step's loads are in flight while the other step's MFMAs run; then the masked tail
+  const int nfull = n & ~15;
+  Ops X, Y;
+  load(2 * kl, X);
+  for (int j0 = 0; j0 < nfull; j0 += 16) {
+    load(j0 + 8 + 2 * kl, Y);
+    mma(X);
+    load(j0 + 16 + 2 * kl, X);
+    mma(Y);
+  }
+  if (nfull < n) {
+    load(nfull + 8 + 2 * kl, Y);
+    ktail(nfull + 2 * kl, X);
+    ktail(nfull + 8 + 2 * kl, Y);
+    mma(X);
+    mma(Y);
+  }
+  // D[row = (λ>>4) + 4·reg][col = λ&15]: row ↔ c, col ↔ i (16 consecutive i per store)
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int c = cw + 16 * t + kl + 4 * reg;
+        const long long i = iw + 16 * u + (lane & 15);
+        if (c < SR && i < Ntest) {
+          const int sm = c / R, l = c - sm * R;
+          gptr_w(T)[(((size_t)sm * D + k) * R + l) * (size_t)Ntest + i] = acc[t][u][reg];
+        }
+      }
+}
+
+// fhat[s·Ntest + i] = Σ_q w_s[q] Π_k T[(s·D + k)·R + I[q,k]][i] for a 64-row tile of sample s.
+template <int R>
+__global__ __launch_bounds__(kNT) void pred_vphase_kernel(const double* __restrict__ w,
+                                                          const double* __restrict__ T,
+                                                          const int32_t* __restrict__ I0, int D,
+                                                          long long Ntest, int Q,
+                                                          double* __restrict__ fhat) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int MP = 65;
+  size_t o = 0;
+  double* temp_l = (double*)(smem + o); o = al16(o + 8 * (size_t)D * R * MP);
+  int* I_l = (int*)(smem + o);          o = al16(o + 4 * (size_t)Q * D);
+  double* w_l = (double*)(smem + o);
+  const int tid = threadIdx.x;
+  const int s = blockIdx.y;
+  const long long i0 = (long long)blockIdx.x * 64;
+  const int Bt = (int)min((long long)64, Ntest - i0);
+  for (int x = tid; x < Q * D; x += kNT) I_l[x] = I0[x];
+  for (int q = tid; q < Q; q += kNT) w_l[q] = w[(size_t)s * Q + q];
+  const double* Ts = T + (size_t)s * D * R * Ntest + i0;
+  for (int x = tid; x < D * R * 64; x += kNT) {
+    const int row = x >> 6, i = x & 63;
+    if (i < Bt) temp_l[row * MP + i] = gptr(Ts)[(size_t)row * Ntest + i];
+  }
+  __syncthreads();
+  vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, I_l, w_l, Q, D, 0, Bt, [&](int comp, int i, double v) {
+    if (comp == 0) fhat[(size_t)s * Ntest + i0 + i] = v;
+  });
+}
+
+// V-phase over the stacked temp with lanes as test rows: one wave = (sample s, 64 rows); the
+// wave stages its D·R temp rows (64 doubles each, coalesced) into LDS, then for every core entry q
+// the D factors temp[k, I[q,k]] are lane-contiguous LDS reads (no bank conflicts) at offsets the
+// whole wave shares, taken from a (q, k) table by scalar loads.
+__global__ void pred_offs_kernel(const int32_t* __restrict__ I0, int Q, int D, int R,
+                                 int32_t* __restrict__ offs) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= Q * D) return;
+  const int q = x / D, k = x - q * D;
+  offs[x] = (int32_t)((k * R + I0[q + Q * k]) * 64);
+}
+
+__global__ __launch_bounds__(64) void pred_vphase_rows_kernel(const double* __restrict__ w,
+                                                              const double* __restrict__ T,
+                                                              const int32_t* __restrict__ offs,
+                                                              int D, int R, long long Ntest,
+                                                              int Q, double* __restrict__ fhat) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* tl = (double*)smem;                       // [k·R + l][64]
+  const int lane = threadIdx.x;
+  const int s = blockIdx.y;
+  const long long i0 = (long long)blockIdx.x * 64;
+  const long long i = i0 + lane;
+  const bool ok = i < Ntest;
+  const double* Ts = T + (size_t)s * D * R * Ntest + (ok ? i : i0);
+  for (int row = 0; row < D * R; ++row) tl[row * 64 + lane] = gptr(Ts)[(size_t)row * Ntest];
+  wave_sync();
+  const auto* ofq = cptr(offs);
+  const auto* wq = cptr(w + (size_t)s * Q);
+  double f0 = 0.0, f1 = 0.0;
+  int q = 0;
+  for (; q + 2 <= Q; q += 2) {
+    double v0 = wq[q], v1 = wq[q + 1];
+    for (int k = 0; k < D; ++k) {
+      v0 *= tl[ofq[q * D + k] + lane];
+      v1 *= tl[ofq[(q + 1) * D + k] + lane];
+    }
+    f0 += v0;
+    f1 += v1;
+  }
+  if (q < Q) {
+    double v0 = wq[q];
+    for (int k = 0; k < D; ++k) v0 *= tl[ofq[q * D + k] + lane];
+    f0 += v0;
+  }
+  if (ok) fhat[(size_t)s * Ntest + i] = f0 + f1;
+}
+
+static size_t pred_vphase_lds_bytes(int D, int r, int Q) {
+  return al16(8 * (size_t)D * r * 65) + al16(4 * (size_t)Q * D) + al16(8 * (size_t)Q);
+}
+
+
+static hipError_t launch_pred_mfma(const double* w, const double* U, const int32_t* I0,
+                                   const double* phitest, int n, int D, long long Ntest, int r,
+                                   int Q, int S, double* fhat, hipStream_t st) {
+  // temp of up to ~1 GiB of samples per pass
+  const size_t per_sample = 8 * (size_t)D * r * (size_t)Ntest;
+  const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)S, ((size_t)1 << 30) / per_sample));
+  double* T = nullptr;
+  const size_t tbytes = (per_sample * chunk + 255) / 256 * 256;
+  hipError_t e = hipMallocAsync((void**)&T, tbytes + 4 * (size_t)Q * D, st);
+  if (e != hipSuccess) return e;
+  int32_t* offs = (int32_t*)((char*)T + tbytes);
+  hipLaunchKernelGGL(pred_offs_kernel, dim3((Q * D + 255) / 256), dim3(256), 0, st, I0, Q, D, r,
+                     offs);
+  const size_t rlds = 8 * (size_t)D * r * 64;
+  static const bool tile_vphase = [] {
+    const char* ev = std::getenv("GPTSGLD_PRED_VPHASE");
+    return ev && std::strcmp(ev, "tile") == 0;
+  }();
+  const size_t vlds = pred_vphase_lds_bytes(D, r, Q);
+  for (int s0 = 0; s0 < S && e == hipSuccess; s0 += chunk) {
+    const int Sc = std::min(chunk, S - s0);
+    const long long total = (long long)((Sc * r + 63) / 64) * ((Ntest + 63) / 64) * D;
+    const unsigned grid = (unsigned)((total + kXcds - 1) / kXcds * kXcds);
+    const double* Us = U + (size_t)s0 * n * r * D;
+    if ((n & 1) == 0)
+      hipLaunchKernelGGL(pred_temp_mfma_kernel<true>, dim3(grid), dim3(256), 0, st, Us, phitest,
+                         n, D, r, Ntest, Sc, T);
+    else
+      hipLaunchKernelGGL(pred_temp_mfma_kernel<false>, dim3(grid), dim3(256), 0, st, Us, phitest,
+                         n, D, r, Ntest, Sc, T);
+    e = hipGetLastError();
+    if (e != hipSuccess) break;
+    dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
+    if (!tile_vphase) {
+      if (rlds > 64 * 1024) {
+        static bool attr = false;
+        if (!attr) {
+          e = hipFuncSetAttribute((const void*)pred_vphase_rows_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+          if (e != hipSuccess) break;
+          attr = true;
+        }
+      }
+      hipLaunchKernelGGL(pred_vphase_rows_kernel, vg, dim3(64), rlds, st, w + (size_t)s0 * Q, T,
+                         offs, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest);
+      e = hipGetLastError();
+      continue;
+    }
+    switch (r) {
+#define CASE(RR)                                                                             \
+  case RR: {                                                                                 \
+    static bool attr = false;                                                                \
+    if (!attr) {                                                                             \
+      e = hipFuncSetAttribute((const void*)pred_vphase_kernel<RR>,                           \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
+      if (e != hipSuccess) break;                                                            \
+      attr = true;                                                                           \
+    }                                                                                        \
+    hipLaunchKernelGGL(pred_vphase_kernel<RR>, vg, dim3(kNT), vlds, st, w + (size_t)s0 * Q, T, \
+                       I0, D, Ntest, Q, fhat + (size_t)s0 * Ntest);                          \
+    e = hipGetLastError();                                                                   \
+  } break;
+      GPT_RANKS(CASE)
+#undef CASE
+      default: e = hipErrorInvalidValue;
+    }
+  }
+  hipError_t ef = hipFreeAsync(T, st);
+  return e != hipSuccess ? e : ef;
+}
+
+static hipError_t launch_pred_direct(const double* w, const double* U, const int32_t* I0, const double* phitest,
                        int n, int D, long long Ntest, int r, int Q, int S, double* fhat,
                        hipStream_t st) {
   if (Ntest <= 0 || S <= 0) return hipSuccess;
@@ -214,6 +498,20 @@ hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, cons
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// Prediction over S stored samples: the MFMA path (stacked-sample GEMM + V-phase) by default;
+// GPTSGLD_PRED=direct selects the per-sample streaming kernel (pred_kernel) for comparison.
+hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, const double* phitest,
+                       int n, int D, long long Ntest, int r, int Q, int S, double* fhat,
+                       hipStream_t st) {
+  if (Ntest <= 0 || S <= 0) return hipSuccess;
+  static const bool direct = [] {
+    const char* ev = std::getenv("GPTSGLD_PRED");
+    return ev && std::strcmp(ev, "direct") == 0;
+  }();
+  if (direct) return launch_pred_direct(w, U, I0, phitest, n, D, Ntest, r, Q, S, fhat, st);
+  return launch_pred_mfma(w, U, I0, phitest, n, D, Ntest, r, Q, S, fhat, st);
 }
 
 hipError_t launch_pred_x(const double* w, const double* U, const int32_t* I0, const double* X,

@@ -101,6 +101,13 @@ class SGLDSession:
                                            C.byref(Us), C.byref(ns)))
         return w.value, U.value, ws.value, Us.value, ns.value
 
+    def gather_state(self, first, count, w_out, U_out):
+        """Current (w, U) of chains first..first+count-1 into device tensors w_out (count, Q) and
+        U_out (count, n*r*D), on the session stream (call sync() before another stream reads)."""
+        check(lib().gpt_sgld_session_gather_state(self._h, first, count,
+                                                  C.c_void_p(w_out.data_ptr()),
+                                                  C.c_void_p(U_out.data_ptr())))
+
     def fetch(self, chain, diag=False):
         """(w_store, U_store, status[, diag]) of one chain, host numpy in Julia layout."""
         ws = np.zeros((self.Q, self.nstore), order="F")

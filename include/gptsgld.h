@@ -130,6 +130,11 @@ int gpt_sgld_session_sync(gpt_sgld_session* s);
 /* Device pointers of chain c's current state and stores (for pred / collectives). */
 int gpt_sgld_session_state(gpt_sgld_session* s, int32_t chain, double** w_dev, double** U_dev,
                            double** w_store_dev, double** U_store_dev, int64_t* nstore);
+/* Current state of chains first .. first+count-1 packed on the device for stacked-sample
+ * prediction (gpt_pred_dev with S = count): w_dev_out (Q, count), U_dev_out (n*r*D, count).
+ * Ordered on the session stream. */
+int gpt_sgld_session_gather_state(gpt_sgld_session* s, int32_t first, int32_t count,
+                                  double* w_dev_out, double* U_dev_out);
 int64_t gpt_sgld_session_steps_done(gpt_sgld_session* s);
 /* Run `nsteps` steps WITHOUT graph capture, bracketing every step-kernel launch with hipEvents;
  * *avg_us = mean step-kernel duration (the roofline's per-launch time).  Synchronises. */

@@ -96,6 +96,29 @@ def test_pred_mean_and_rmse():
     assert rm == pytest.approx(R.rmse(p["y"], want, 2.5), rel=1e-10)
 
 
+@pytest.mark.parametrize("n,D,Nt,r,Q,S", [
+    (41, 3, 200, 5, 30, 30),       # odd n (8-B operand loads), 3 c-tiles of the S·r GEMM, ragged rows
+    (150, 8, 130, 20, 200, 4),     # the reference's kin40k rank (r = 20, n = 150)
+    (500, 8, 700, 5, 200, 40),     # bench shape, 4 c-tiles, 11 row tiles
+])
+def test_pred_stacked_samples_mfma(n, D, Nt, r, Q, S):
+    """pred over S stacked samples (fp64-MFMA phidotU GEMM M = S·r, N = Ntest, K = n, then the
+    V-phase) against the oracle's pred of every sample."""
+    rng = np.random.default_rng(n + S)
+    X = rng.standard_normal((Nt, D)); Z = rng.standard_normal((n, D)); b = 2 * np.pi * rng.random((n, D))
+    phi = R.feature(X, 1.0 + 0.1 * rng.random(D), 1.0, math.sqrt(n / Q ** (1.0 / D)), Z, b)
+    I = R.samplenz(r, D, Q, 5)
+    ws = rng.standard_normal((Q, S))
+    Us = np.stack([R.init_state(n, r, D, Q, 50 + s)[1] for s in range(S)], axis=3)
+    yt = rng.standard_normal(Nt)
+    mean, rm = G().pred_mean(ws, Us.reshape((n, r, D * S), order="F"), I, phi, yt, scale=1.3)
+    f = np.stack([R.pred(ws[:, s], Us[..., s], I, phi) for s in range(S)])
+    assert rel(mean, f.mean(axis=0)) < 1e-12
+    assert rm == pytest.approx(R.rmse(yt, f.mean(axis=0), 1.3), rel=1e-10)
+    f1 = G().pred(ws[:, S - 1], Us[..., S - 1], I, phi)
+    assert rel(f1, f[S - 1]) < 1e-12
+
+
 # ----------------------------------------------------------------------------- sampler
 CASES = {
     # name: (n, D, N, r, Q, m, burnin, maxepoch, store_every, langevin, stiefel)
@@ -205,7 +228,8 @@ def test_pred_mean_x_fused_features():
                                     2.0, Z, b, scale=1.7)
     phi = G().feature(X, ls, 1.1, 2.0, Z, b)
     mean2, rm2 = G().pred_mean(ws, Us.reshape((n, r, D * S), order="F"), I, phi, yt, scale=1.7)
-    assert rel(mean, mean2) < 1e-15 and abs(rm - rm2) <= 1e-15 * rm2
+    # pred_mean runs the stacked-sample MFMA GEMM (another summation order than the fused tile)
+    assert rel(mean, mean2) < 1e-13 and abs(rm - rm2) <= 1e-13 * rm2
     phio = R.feature(X, ls, 1.1, 2.0, Z, b)
     f = np.stack([R.pred(ws[:, s], Us[..., s], I, phio) for s in range(S)])
     assert rel(mean, f.mean(axis=0)) < 1e-12
