@@ -1024,10 +1024,27 @@ extern "C" int gpt_pred_mean_x(const double* w_store, const double* U_store, con
   HIPCHK(hipMemcpy(dZ.p, Z, 8 * (size_t)n * D, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(db.p, b, 8 * (size_t)n * D, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dy.p, ytest, 8 * (size_t)Ntest, hipMemcpyHostToDevice));
-  hipError_t e = launch_pred_x(dw.as<double>(), dU.as<double>(), dI.as<int32_t>(), dX.as<double>(),
-                               dls.as<double>(), dZ.as<double>(), db.as<double>(), c, (int)n, (int)D,
-                               Ntest, (int)r, (int)Q, (int)S, df.as<double>(), nullptr);
-  if (e != hipSuccess) return hip_fail(e, "pred_x kernel");
+  // Default: the test features are formed once on the device (feature_kernel, the same doubles
+  // as gpt_feature) and every sample is predicted by the stacked-sample MFMA path, which reads
+  // them through L2 per group of samples.  GPTSGLD_PRED=direct: pred_x_kernel, which forms the
+  // features inside every sample's prediction tile (no phitest array).
+  const char* pev = std::getenv("GPTSGLD_PRED");
+  hipError_t e;
+  DevMem dphi;
+  if (pev && std::strcmp(pev, "direct") == 0) {
+    e = launch_pred_x(dw.as<double>(), dU.as<double>(), dI.as<int32_t>(), dX.as<double>(),
+                      dls.as<double>(), dZ.as<double>(), db.as<double>(), c, (int)n, (int)D,
+                      Ntest, (int)r, (int)Q, (int)S, df.as<double>(), nullptr);
+    if (e != hipSuccess) return hip_fail(e, "pred_x kernel");
+  } else {
+    HIPCHK(dphi.alloc(8 * (size_t)n * D * Ntest));
+    e = launch_feature(dX.as<double>(), Ntest, (int)D, dls.as<double>(), c, dZ.as<double>(),
+                       db.as<double>(), (int)n, dphi.as<double>(), nullptr);
+    if (e != hipSuccess) return hip_fail(e, "feature kernel");
+    e = launch_pred(dw.as<double>(), dU.as<double>(), dI.as<int32_t>(), dphi.as<double>(), (int)n,
+                    (int)D, Ntest, (int)r, (int)Q, (int)S, df.as<double>(), nullptr);
+    if (e != hipSuccess) return hip_fail(e, "pred kernels");
+  }
   e = launch_mean_rmse(df.as<double>(), dy.as<double>(), Ntest, (int)S, dmean.as<double>(),
                        dsse.as<double>(), nullptr);
   if (e != hipSuccess) return hip_fail(e, "mean/sse kernel");

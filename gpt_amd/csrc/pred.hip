@@ -209,15 +209,16 @@ typedef double pd4 __attribute__((ext_vector_type(4)));
 typedef double pd2 __attribute__((ext_vector_type(2)));
 constexpr int kXcds = 8;
 
-template <bool V2>
+template <bool V2, int TM, int TN>
 __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __restrict__ U,
                                                              const double* __restrict__ phi,
                                                              int n, int D, int R,
                                                              long long Ntest, int S,
                                                              double* __restrict__ T) {
+  constexpr int WC = 32 * TM, WI = 32 * TN;        // workgroup tile (2 × 2 waves of 16TM × 16TN)
   const int SR = S * R;
-  const int nct = (SR + 63) / 64;
-  const long long nit = (Ntest + 63) / 64;
+  const int nct = (SR + WC - 1) / WC;
+  const long long nit = (Ntest + WI - 1) / WI;
   const long long total = (long long)nct * nit * D;
   const long long per = ((long long)gridDim.x) / kXcds;
   const long long logical = (long long)(blockIdx.x % kXcds) * per + blockIdx.x / kXcds;
@@ -227,23 +228,26 @@ __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __res
   const long long it = rest % nit;
   const int k = (int)(rest / nit);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, kl = lane >> 4;
-  const int cw = ct * 64 + (wv & 1) * 32;
-  const long long iw = it * 64 + (wv >> 1) * 32;
-  const __attribute__((address_space(1))) double* pa[2];
-  const __attribute__((address_space(1))) double* pb[2];
+  const int cw = ct * WC + (wv & 1) * 16 * TM;
+  const long long iw = it * WI + (wv >> 1) * 16 * TN;
+  const __attribute__((address_space(1))) double* pa[TM];
+  const __attribute__((address_space(1))) double* pb[TN];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < TM; ++t) {
     const int c = cw + 16 * t + (lane & 15);
     const int cc = c < SR ? c : 0, sm = cc / R, l = cc - sm * R;
     pa[t] = gptr(U + (size_t)sm * n * R * D + (size_t)n * (l + R * k));
-    const long long i = iw + 16 * t + (lane & 15);
-    pb[t] = gptr(phi + (size_t)n * (k + (size_t)D * (i < Ntest ? i : 0)));
   }
-  pd4 acc[2][2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int u = 0; u < TN; ++u) {
+    const long long i = iw + 16 * u + (lane & 15);
+    pb[u] = gptr(phi + (size_t)n * (k + (size_t)D * (i < Ntest ? i : 0)));
+  }
+  pd4 acc[TM][TN];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) acc[t][u] = pd4{0.0, 0.0, 0.0, 0.0};
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u) acc[t][u] = pd4{0.0, 0.0, 0.0, 0.0};
   // Branch- and select-free operand loads in the K loop (address clamped in-row): lanes of
   // columns c >= S·R or rows i >= Ntest read row 0 and only feed outputs that are never stored,
   // so the loaded values go straight into the MFMAs and the loads of one step stay in flight
@@ -257,33 +261,32 @@ __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __res
       x1 = p[min(j + 1, n - 1)];
     }
   };
-  struct Ops { double a0[2], a1[2], b0[2], b1[2]; };
+  struct Ops { double a0[TM], a1[TM], b0[TN], b1[TN]; };
   auto load = [&](int j, Ops& o) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      ld(pa[t], j, o.a0[t], o.a1[t]);
-      ld(pb[t], j, o.b0[t], o.b1[t]);
-    }
+    for (int t = 0; t < TM; ++t) ld(pa[t], j, o.a0[t], o.a1[t]);
+#pragma unroll
+    for (int u = 0; u < TN; ++u) ld(pb[u], j, o.b0[u], o.b1[u]);
   };
   auto ktail = [&](int j, Ops& o) {    // zero the A halves past n (one operand suffices)
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < TM; ++t) {
       o.a0[t] = j < n ? o.a0[t] : 0.0;
       o.a1[t] = j + 1 < n ? o.a1[t] : 0.0;
     }
   };
-  // the four independent accumulators with the even K half, then with the odd one (no
-  // back-to-back MFMA on one accumulator)
+  // every accumulator with the even K half, then with the odd one (TM·TN >= 4 independent MFMAs
+  // between two on one accumulator)
   auto mma = [&](const Ops& o) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < TN; ++u)
         acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.a0[t], o.b0[u], acc[t][u], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < TN; ++u)
         acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.a1[t], o.b1[u], acc[t][u], 0, 0, 0);
   };
   // two K steps of 8 per iteration over the full 16-blocks, ping-ponging two operand sets: one
@@ -306,9 +309,9 @@ __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __res
   }
   // D[row = (λ>>4) + 4·reg][col = λ&15]: row ↔ c, col ↔ i (16 consecutive i per store)
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < TM; ++t)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < TN; ++u)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
         const int c = cw + 16 * t + kl + 4 * reg;
@@ -403,6 +406,33 @@ static size_t pred_vphase_lds_bytes(int D, int r, int Q) {
 }
 
 
+// Workgroup tile of the stacked-sample GEMM: GPTSGLD_PRED_TILE = "22" (64 × 64, default "44")
+// selects the wave tile (16·TM c × 16·TN i) for comparison runs.
+template <int TM, int TN>
+static void launch_pred_gemm_t(const double* Us, const double* phitest, int n, int D, int r,
+                               long long Ntest, int Sc, double* T, hipStream_t st) {
+  const long long total = (long long)((Sc * r + 32 * TM - 1) / (32 * TM)) *
+                          ((Ntest + 32 * TN - 1) / (32 * TN)) * D;
+  const unsigned grid = (unsigned)((total + kXcds - 1) / kXcds * kXcds);
+  if ((n & 1) == 0)
+    hipLaunchKernelGGL((pred_temp_mfma_kernel<true, TM, TN>), dim3(grid), dim3(256), 0, st, Us,
+                       phitest, n, D, r, Ntest, Sc, T);
+  else
+    hipLaunchKernelGGL((pred_temp_mfma_kernel<false, TM, TN>), dim3(grid), dim3(256), 0, st, Us,
+                       phitest, n, D, r, Ntest, Sc, T);
+}
+
+static hipError_t launch_pred_gemm(const double* Us, const double* phitest, int n, int D, int r,
+                                   long long Ntest, int Sc, double* T, hipStream_t st) {
+  const char* ev = std::getenv("GPTSGLD_PRED_TILE");
+  const int tile = ev ? std::atoi(ev) : 44;
+  if (tile == 22) launch_pred_gemm_t<2, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st);
+  else if (tile == 42) launch_pred_gemm_t<4, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st);
+  else if (tile == 24) launch_pred_gemm_t<2, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st);
+  else launch_pred_gemm_t<4, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st);
+  return hipGetLastError();
+}
+
 static hipError_t launch_pred_mfma(const double* w, const double* U, const int32_t* I0,
                                    const double* phitest, int n, int D, long long Ntest, int r,
                                    int Q, int S, double* fhat, hipStream_t st) {
@@ -424,16 +454,8 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
   const size_t vlds = pred_vphase_lds_bytes(D, r, Q);
   for (int s0 = 0; s0 < S && e == hipSuccess; s0 += chunk) {
     const int Sc = std::min(chunk, S - s0);
-    const long long total = (long long)((Sc * r + 63) / 64) * ((Ntest + 63) / 64) * D;
-    const unsigned grid = (unsigned)((total + kXcds - 1) / kXcds * kXcds);
     const double* Us = U + (size_t)s0 * n * r * D;
-    if ((n & 1) == 0)
-      hipLaunchKernelGGL(pred_temp_mfma_kernel<true>, dim3(grid), dim3(256), 0, st, Us, phitest,
-                         n, D, r, Ntest, Sc, T);
-    else
-      hipLaunchKernelGGL(pred_temp_mfma_kernel<false>, dim3(grid), dim3(256), 0, st, Us, phitest,
-                         n, D, r, Ntest, Sc, T);
-    e = hipGetLastError();
+    e = launch_pred_gemm(Us, phitest, n, D, r, Ntest, Sc, T, st);
     if (e != hipSuccess) break;
     dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
     if (!tile_vphase) {
