@@ -780,7 +780,7 @@ def tgp_V(U, I, b):
 
 
 def GPT_inf(b, y, sigma, n, r, q, num_iterations, burnin, seed, I=None):
-    """TGP.jl:37-86 (Gibbs sweep of the tensor GP) on whitened data: ``b`` (n, D, N) is the
+    r"""TGP.jl:37-86 (Gibbs sweep of the tensor GP) on whitened data: ``b`` (n, D, N) is the
     feature array of TGP.feature (TGP.jl:6-14) and ``y`` (N) the whitened targets.
 
     Per sweep: W ~ N(Mu_w, invSigma_w⁻¹) through the upper Cholesky factor (:57-59); for each k

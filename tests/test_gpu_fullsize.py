@@ -1,0 +1,117 @@
+"""Full-size properties of the benchmark workload (kin40k: N = 10 000, D = 8, n = 500, r = 5,
+Q = 200, m = 50, 256 chains = the bench's chain engine launch), where the oracle is too slow to
+follow every chain:
+
+  * one chain of the 256-chain launch equals the oracle's GPTregression on the same seed
+    (GPT_SGLD.jl:345-448) for the first steps (trajectory tolerance 1e-8 as tests/test_gpu_parity.py);
+  * chains are independent: chain c of the 256-chain session equals a 1-chain session of its seed
+    (bitwise: a chain's arithmetic does not depend on its neighbours);
+  * the run is deterministic: two sessions give bitwise-identical states;
+  * U stays on the Stiefel manifold (UᵀU = I per dimension, |Δ| <= 1e-12) for every chain (geod,
+    GPT_SGLD.jl:19-37, renormalises the columns; orthogonality is kept by the geodesic);
+  * the stacked-sample prediction of all 256 final states equals per-sample predictions
+    (pred, :233-243) of the same states through the oracle for a subset of rows.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import gpt_sgld_ref as R
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+n, D, r, Q, m = 500, 8, 5, 200, 50
+EPSW, EPSU, SV = 1e-5, 1e-8, 0.0476
+STEPS = 6
+
+
+def rel(a, b):
+    a = np.asarray(a); b = np.asarray(b)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def problem():
+    import torch
+    import bench
+    from gpt_amd import GPT_SGLD as G
+    from gpt_amd.session import feature_device
+    Xtr, ytr, Xte, yte, _ = bench.kin40k(D)
+    ls = np.array([2.5242, 2.3376, 1.3630, 1.4949, 1.6022, 1.1366, 1.1964, 1.7028])
+    scale = math.sqrt(n / Q ** (1.0 / D))
+    I = G.samplenz(r, D, Q, 17)
+    Z, b = G.feature_inputs(n, D, 17)
+    dev = torch.device("cuda", 0)
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    phi = feature_device(tt(Xtr.T), tt(ls), 1.0420, scale, tt(Z.T), tt(b.T))
+    phi_te = feature_device(tt(Xte[:512].T), tt(ls), 1.0420, scale, tt(Z.T), tt(b.T))
+    torch.cuda.synchronize()
+    return dict(phi=phi, y=tt(ytr), ytr=ytr, I=I, phi_te=phi_te)
+
+
+def run_session(p, seeds, steps=STEPS):
+    from gpt_amd.session import SGLDSession
+    s = SGLDSession(p["phi"], p["y"], p["I"], r, Q, m, EPSW, EPSU, SV, 0, 1, seeds, store=True,
+                    engine="chain")
+    assert s.info()["engine"] == "chain"
+    s.run(steps)
+    s.sync()
+    return s
+
+
+def test_fullsize_chain_matches_oracle_and_single_runs(problem):
+    import torch
+    seeds = list(range(1, 257))
+    s = run_session(problem, seeds)
+    probe = [0, 97, 255]
+    states = {c: s.fetch(c) for c in probe}
+    for c in probe:
+        assert states[c][2] == 0
+    # independence: the same seed alone
+    for c in (0, 255):
+        s1 = run_session(problem, [seeds[c]])
+        ws1, Us1, st1 = s1.fetch(0)
+        s1.close()
+        assert st1 == 0
+        assert np.array_equal(ws1[:, :STEPS], states[c][0][:, :STEPS])
+        assert np.array_equal(Us1[..., :STEPS], states[c][1][..., :STEPS])
+    # determinism
+    s2 = run_session(problem, seeds)
+    ws2, Us2, _ = s2.fetch(97)
+    s2.close()
+    assert np.array_equal(ws2[:, :STEPS], states[97][0][:, :STEPS])
+    assert np.array_equal(Us2[..., :STEPS], states[97][1][..., :STEPS])
+    # oracle on one chain (host copy of the device features, Julia layout (n, D, N))
+    phi_np = np.asfortranarray(problem["phi"].cpu().numpy().transpose(2, 1, 0))
+    wo, Uo, _ = R.GPTregression(phi_np, problem["ytr"], SV, problem["I"], r, Q, m, EPSW, EPSU, 0, 1,
+                                seeds[97], max_steps=STEPS)
+    assert rel(states[97][0][:, :STEPS], wo[:, :STEPS]) < 1e-8
+    assert rel(states[97][1][..., :STEPS], Uo[..., :STEPS]) < 1e-8
+    # Stiefel invariant for every chain's current U
+    nrD = n * r * D
+    w_all = torch.empty((256, Q), dtype=torch.float64, device="cuda")
+    U_all = torch.empty((256, nrD), dtype=torch.float64, device="cuda")
+    s.gather_state(0, 256, w_all, U_all)
+    s.sync()
+    Ut = U_all.view(256, D, r, n)                     # Julia U[j, l, k] at j + n(l + r k)
+    gram = torch.einsum("ckaj,ckbj->ckab", Ut, Ut)
+    eye = torch.eye(r, dtype=torch.float64, device="cuda")
+    assert (gram - eye).abs().max().item() <= 1e-12
+    # stacked-sample prediction of all final states vs the oracle's per-sample pred on a row subset
+    from gpt_amd.session import pred_device
+    I0 = torch.from_numpy(np.asfortranarray(problem["I"] - 1).ravel(order="F").astype(np.int32)).cuda()
+    Nt = problem["phi_te"].shape[0]
+    fh = torch.empty((256, Nt), dtype=torch.float64, device="cuda")
+    pred_device(w_all.data_ptr(), U_all.data_ptr(), I0, problem["phi_te"], n, D, Nt, r, Q, 256, fh)
+    torch.cuda.synchronize()
+    fh = fh.cpu().numpy()
+    phi_te_np = np.asfortranarray(problem["phi_te"].cpu().numpy().transpose(2, 1, 0))
+    wn, Un = w_all.cpu().numpy(), U_all.cpu().numpy()
+    for c in (0, 97, 255):
+        Uc = Un[c].reshape((n, r, D), order="F")
+        want = R.pred(wn[c], Uc, problem["I"], phi_te_np)
+        assert rel(fh[c], want) < 1e-12
+    s.close()
