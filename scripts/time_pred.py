@@ -1,7 +1,8 @@
 """Time the stacked-sample prediction (MFMA GEMM + V-phase) per GEMM wave tile on the GPU.
 
     python scripts/time_pred.py [--S 256] [--n 500] [--r 5] [--Ntest 30000]
-Prints ms per call and the GEMM's fp64 TFLOP/s for GPTSGLD_PRED_TILE = 22, 42, 24, 44.
+Prints ms per call and the GEMM's fp64 TFLOP/s for each GPTSGLD_PRED_TILE (22, 42, 24, 44) and
+GPTSGLD_PRED_VPHASE (rows, tile) combination asked for.
 """
 import argparse
 import os
@@ -23,6 +24,7 @@ def main():
     ap.add_argument("--Ntest", type=int, default=30000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tiles", default="22,42,24,44")
+    ap.add_argument("--vphases", default="rows", help="GPTSGLD_PRED_VPHASE values to compare (rows, tile)")
     a = ap.parse_args()
     import torch
     from gpt_amd import GPT_SGLD as G
@@ -37,8 +39,9 @@ def main():
     f = torch.empty(a.S, a.Ntest, dtype=torch.float64, device=dev)
     flop = 2.0 * a.S * a.r * a.n * a.D * a.Ntest
     ref = None
-    for tile in a.tiles.split(","):
+    for tile, vp in [(t, v) for t in a.tiles.split(",") for v in a.vphases.split(",")]:
         os.environ["GPTSGLD_PRED_TILE"] = tile
+        os.environ["GPTSGLD_PRED_VPHASE"] = vp
         pred_device(w.data_ptr(), U.data_ptr(), I0, phi, a.n, a.D, a.Ntest, a.r, a.Q, a.S, f)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -51,8 +54,8 @@ def main():
         if ref is None:
             ref = f.clone()
         d = (f - ref).abs().max().item() / ref.abs().max().item()
-        print("tile %s: %.3f ms per call (GEMM + V-phase), GEMM flop / call time %.1f TFLOP/s, "
-              "max rel diff vs first tile %.1e" % (tile, ms, flop / ms / 1e9, d), flush=True)
+        print("tile %s vphase %s: %.3f ms per call (GEMM + V-phase), GEMM flop / call time %.1f "
+              "TFLOP/s, max rel diff vs the first %.1e" % (tile, vp, ms, flop / ms / 1e9, d), flush=True)
 
 
 if __name__ == "__main__":
