@@ -41,6 +41,25 @@ def kin40k(D):
     return Xtr[:, :D], (ytr - ymu) / ysd, Xte[:, :D], (yte - ymu) / ysd, ysd
 
 
+def powerplant(D, ntrain=5000):
+    """BASELINE config 2 (SURVEY §8 canonical shapes): Folds5x2_pp.csv rows 1..5000 train, the
+    other 4568 test, whitened with the train moments as PowerPlantDataExperiment.jl:25-37."""
+    d = np.load(os.path.join(ROOT, "tests", "golden", "powerplant.npz"))["data"]
+    Xtr, ytr, Xte, yte = d[:ntrain, :D], d[:ntrain, D], d[ntrain:, :D], d[ntrain:, D]
+    mu, sd = Xtr.mean(axis=0), Xtr.std(axis=0, ddof=1)
+    ymu, ysd = ytr.mean(), ytr.std(ddof=1)
+    return (Xtr - mu) / sd, (ytr - ymu) / ysd, (Xte - mu) / sd, (yte - ymu) / ysd, ysd
+
+
+WORKLOADS = {
+    # name: (loader, D, minibatch, length scales, sigma_RBF, signal_var, description)
+    "kin40k": (kin40k, 8, 50, [2.5242, 2.3376, 1.3630, 1.4949, 1.6022, 1.1366, 1.1964, 1.7028],
+               1.0420, 0.0476, "kin40k tensor-GP SGLD (GPTregression)"),
+    "powerplant": (powerplant, 4, 256, [1.4332] * 4, 1.0, 0.2299 ** 2,
+                   "PowerPlant tensor-GP SGLD (GPTregression), BASELINE config 2"),
+}
+
+
 def algorithmic_bytes_per_step(n, D, B, r, Q):
     """8·(n·D·B + B + 2·n·r·D + 2·Q) + 4·Q·D bytes per SGLD step."""
     return 8 * (n * D * B + B + 2 * n * r * D + 2 * Q) + 4 * Q * D
@@ -77,9 +96,9 @@ def cpu_baseline(phi_np, y_np, I, args, seconds):
         if ctx:
             ctx.__exit__(None, None, None)
     return dict(value=steps / dt, unit="SGLD steps/s (1 chain)", cores=1, kind="port",
-                sample="oracle/gpt_sgld_ref.py GPTregression, %d steps of the kin40k config "
+                sample="oracle/gpt_sgld_ref.py GPTregression, %d steps of the %s config "
                        "(n=%d, D=%d, r=%d, Q=%d, m=%d), numpy fp64, 1 BLAS thread, %.1f s incl. init"
-                       % (steps, args.n, args.D, args.r, args.Q, args.m, dt))
+                       % (steps, args.workload, args.n, args.D, args.r, args.Q, args.m, dt))
 
 
 def main():
@@ -89,19 +108,21 @@ def main():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--chains", type=int, default=0,
                     help="independent chains per GPU (0: one per CU for the chain engine, "
-                         "28 (x D+1 workgroups) for the grid engine)")
+                         "CUs // (D+1) for the grid engine, D+1 workgroups per chain)")
     ap.add_argument("--engine", default="auto", choices=["auto", "grid", "chain"])
+    ap.add_argument("--workload", default="kin40k", choices=sorted(WORKLOADS),
+                    help="kin40k (BASELINE configs 3/4, the metric's workload) or powerplant (config 2)")
     ap.add_argument("--n", type=int, default=500)
-    ap.add_argument("--D", type=int, default=8)
+    ap.add_argument("--D", type=int, default=None, help="default: the workload's D (8 / 4)")
     ap.add_argument("--r", type=int, default=5)
     ap.add_argument("--Q", type=int, default=200)
-    ap.add_argument("--m", type=int, default=50)
+    ap.add_argument("--m", type=int, default=None, help="minibatch (default: 50 / 256)")
     # kin40kExperiment.jl:50-51 uses εw=1e-4, εU=1e-7 at n=150, r=20; under the restated
     # GPT_SGLD.jl update both the oracle and the GPU path diverge there (w Hessian λmax≈3e5),
     # so the benchmark uses the largest stable pair found by the oracle sweep.
     ap.add_argument("--epsw", type=float, default=1e-5)
     ap.add_argument("--epsU", type=float, default=1e-8)
-    ap.add_argument("--signal_var", type=float, default=0.0476)
+    ap.add_argument("--signal_var", type=float, default=None, help="default: the workload's")
     ap.add_argument("--kernel-steps", type=int, default=100, help="steps of the event-timed pass")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -109,6 +130,13 @@ def main():
                     help="skip the C=1 latency pass (one chain on one CU)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
+    loader, wD, wm, wls, sigma_rbf, wsv, wdesc = WORKLOADS[args.workload]
+    if args.D is None:
+        args.D = wD
+    if args.m is None:
+        args.m = wm
+    if args.signal_var is None:
+        args.signal_var = wsv
 
     import torch
     import torch.distributed as dist
@@ -124,10 +152,9 @@ def main():
     from gpt_amd.session import SGLDSession, feature_device, pred_device
 
     n, D, r, Q, m = args.n, args.D, args.r, args.Q, args.m
-    Xtr, ytr, Xte, yte, ysd = kin40k(D)
+    Xtr, ytr, Xte, yte, ysd = loader(D)
     N, Nte = Xtr.shape[0], Xte.shape[0]
-    ls = np.array([2.5242, 2.3376, 1.3630, 1.4949, 1.6022, 1.1366, 1.1964, 1.7028])[:D]
-    sigma_rbf = 1.0420
+    ls = np.array(wls)[:D]
     scale = math.sqrt(n / Q ** (1.0 / D))                 # kin40kExperiment.jl:45
     I = G.samplenz(r, D, Q, 17)                           # :44 (seed 17)
     Z, b = G.feature_inputs(n, D, 17)                     # Gen-C seeded feature inputs
@@ -144,7 +171,8 @@ def main():
                             [1], store=False, engine=args.engine)
         eng = probe.info()["engine"]
         probe.close()
-        C = torch.cuda.get_device_properties(dev).multi_processor_count if eng == "chain" else 28
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        C = cus if eng == "chain" else max(1, cus // (D + 1))   # grid: D+1 workgroups per chain
     need = args.warmup + args.steps + args.kernel_steps
     epochs = -(-need // nb) + 1
     seeds = [1000 * rank + c + 1 for c in range(C)]
@@ -231,7 +259,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "SGLD steps/sec (kin40k, n_feat=500/dim, r=5)",
+            "metric": ("SGLD steps/sec (kin40k, n_feat=500/dim, r=5)" if args.workload == "kin40k"
+                       else "SGLD steps/sec (PowerPlant, n_feat=500/dim, r=5, minibatch 256)"),
             "value": value,
             "unit": "chain-steps/s",
             "n_gpus": world,
@@ -242,8 +271,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "kin40k reference files (tests/golden/kin40k.npz), whitened; features on device",
-            "config": {"workload": "kin40k tensor-GP SGLD (GPTregression)", "Ntrain": N, "Ntest": Nte,
+            "data": ("%s reference files (tests/golden/%s.npz), whitened; features on device"
+                     % (args.workload, args.workload)),
+            "config": {"workload": wdesc, "Ntrain": N, "Ntest": Nte,
                        "D": D, "n_features": n, "r": r, "Q": Q, "minibatch": m,
                        "chains_per_gpu": C, "epsw": args.epsw, "epsU": args.epsU,
                        "signal_var": args.signal_var, "parallelism": "chains%dx%d" % (C, world),
