@@ -122,8 +122,11 @@ __device__ __forceinline__ void wave_sum_to_lds(double (&v)[2 * NV], double* dst
   }
 }
 
-template <int R, int J, int G>
-__global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
+// WV: waves per workgroup the build is bounded for — kChainDMax, or 4 for D <= 4, where one wave
+// per SIMD leaves the register file to two V tasks per wave even at J = 8 (PowerPlant, D = 4,
+// minibatch 256: 8 tasks per row group).
+template <int R, int J, int G, int WV>
+__global__ __launch_bounds__(64 * WV) void chain_kernel(StepParams P,
                                                                 const ChainDesc* chains,
                                                                 const long long* __restrict__ tbase,
                                                                 int t_local) {
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(64 * kChainDMax) void chain_kernel(StepParams P,
   for (int jj = 0; jj < J; ++jj)
 #pragma unroll
     for (int l = 0; l < R; ++l) acc[jj][l] = 0.0;
-  constexpr int TPW = J >= 8 ? 1 : kChainTasks;   // register budget: one task per wave at J = 8
+  constexpr int TPW = (J >= 8 && WV > 4) ? 1 : kChainTasks;   // one task per wave at J = 8, D > 4
   double vsave[TPW], gw[TPW];
 #pragma unroll
   for (int x = 0; x < TPW; ++x) { vsave[x] = 0.0; gw[x] = 0.0; }
@@ -686,7 +689,7 @@ bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stie
   if (chain_J(n) >= 2 && (n & 1)) return false;   // 16-B row staging needs 16-B aligned rows
   if (Q > kChainQP || m > kChainMMax) return false;   // the fixed LDS carve's maxima
   const int NT = (Q + 63) / 64 * kChainG;
-  if (NT > (chain_J(n) >= 8 ? 1 : kChainTasks) * D) return false;
+  if (NT > ((chain_J(n) >= 8 && D > 4) ? 1 : kChainTasks) * D) return false;
   return chain_lds_bytes(n, D, r, Q, m) + chain_static_lds(chain_J(n)) <= 160 * 1024;
 }
 
@@ -695,21 +698,24 @@ hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchain
   const int J = chain_J(P.n);
   const size_t lds = chain_lds_bytes(P.n, P.D, P.r, P.Q, P.m);
   dim3 grid(nchains), block(64 * P.D);
-#define CASE(RR, JJ)                                                                          \
-  if (P.r == RR && J == JJ) {                                                                 \
+#define CASE_W(RR, JJ, WW)                                                                    \
+  if (P.r == RR && J == JJ && (P.D <= 4) == (WW == 4)) {                                      \
     static bool attr = false;                                                                 \
     if (!attr) {                                                                              \
-      hipError_t e = hipFuncSetAttribute((const void*)chain_kernel<RR, JJ, kChainG>,          \
+      hipError_t e = hipFuncSetAttribute((const void*)chain_kernel<RR, JJ, kChainG, WW>,      \
                                          hipFuncAttributeMaxDynamicSharedMemorySize,          \
                                          (int)(160 * 1024 - chain_static_lds(JJ)));           \
       if (e != hipSuccess) return e;                                                          \
       attr = true;                                                                            \
     }                                                                                         \
-    hipLaunchKernelGGL((chain_kernel<RR, JJ, kChainG>), grid, block, lds, st, P, chains, tbase, t_local); \
+    hipLaunchKernelGGL((chain_kernel<RR, JJ, kChainG, WW>), grid, block, lds, st, P, chains, tbase, \
+                       t_local);                                                              \
     return hipGetLastError();                                                                 \
   }
+#define CASE(RR, JJ) CASE_W(RR, JJ, kChainDMax) CASE_W(RR, JJ, 4)
   GPT_CHAIN_CFGS(CASE)
 #undef CASE
+#undef CASE_W
   return hipErrorInvalidValue;
 }
 

@@ -131,6 +131,7 @@ CASES = {
     "rank10": (100, 4, 120, 10, 60, 30, 0, 1, 1, True, True),
     "ref_kin40k_rank20": (150, 8, 100, 20, 200, 50, 0, 1, 1, True, True),
     "batch256": (96, 4, 600, 5, 80, 256, 0, 1, 1, True, True),
+    "powerplant_shape": (500, 4, 600, 5, 200, 256, 0, 2, 1, True, True),   # D <= 4 build, J = 8, 2 V tasks/wave
 }
 
 
