@@ -237,6 +237,8 @@ def main():
     pred_flop = 2.0 * npred * r * n * D * Nte             # the GEMM (dominant); V-phase excluded
     fsum = fh.sum(dim=0)
     from gpt_amd.ensemble import combine_predictive_mean, rmse as ens_rmse
+    combine_predictive_mean(torch.zeros_like(fsum), 1)   # warm-up (communicator setup, kernels)
+    torch.cuda.synchronize()
     ta = time.perf_counter()
     fmean = combine_predictive_mean(fsum, npred)     # RCCL all-reduce across ranks (config 4)
     torch.cuda.synchronize()
