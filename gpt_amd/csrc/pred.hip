@@ -436,9 +436,16 @@ static hipError_t launch_pred_gemm(const double* Us, const double* phitest, int 
 static hipError_t launch_pred_mfma(const double* w, const double* U, const int32_t* I0,
                                    const double* phitest, int n, int D, long long Ntest, int r,
                                    int Q, int S, double* fhat, hipStream_t st) {
-  // temp of up to ~1 GiB of samples per pass
+  // temp of up to ~2 GiB of samples per pass; a pass of several workgroup tiles takes a multiple of
+  // 128 / gcd(128, r) samples, so its S·r columns fill whole 128-column tiles (no MFMA padding)
   const size_t per_sample = 8 * (size_t)D * r * (size_t)Ntest;
-  const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)S, ((size_t)1 << 30) / per_sample));
+  int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)S, ((size_t)2 << 30) / per_sample));
+  {
+    int g = 128, b = r;
+    while (b) { const int t = g % b; g = b; b = t; }
+    const int unit = 128 / g;
+    if (chunk < S && chunk >= unit) chunk = chunk / unit * unit;
+  }
   double* T = nullptr;
   const size_t tbytes = (per_sample * chunk + 255) / 256 * 256;
   hipError_t e = hipMallocAsync((void**)&T, tbytes + 4 * (size_t)Q * D, st);
