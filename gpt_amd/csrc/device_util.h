@@ -332,6 +332,40 @@ __constant__ double kPade[4][10] = {
 template <int NN>
 __device__ __forceinline__ void wave_mm(const double* A, const double* B, double* C) {
   const int lane = threadIdx.x & 63;
+  if constexpr (NN >= 16) {
+    // register-blocked: lane (bi, bj) of an NB × NB grid owns a BS × BS block of C, so each LDS
+    // value read feeds BS FMAs (NN = 40: 5 × 5 blocks, 0.4 reads per FMA instead of 2).  Every
+    // output is still Σ_t A[i,t]·B[t,j] accumulated in t order — the same doubles as below.
+    constexpr int BS = (NN + 7) / 8, NB = (NN + BS - 1) / BS;
+    if (lane < NB * NB) {
+      const int i0 = (lane / NB) * BS, j0 = (lane % NB) * BS;
+      double acc[BS][BS];
+#pragma unroll
+      for (int x = 0; x < BS; ++x)
+#pragma unroll
+        for (int y = 0; y < BS; ++y) acc[x][y] = 0.0;
+#pragma unroll 4
+      for (int t = 0; t < NN; ++t) {
+        double a[BS], b[BS];
+#pragma unroll
+        for (int x = 0; x < BS; ++x) {
+          a[x] = A[min(i0 + x, NN - 1) * NN + t];
+          b[x] = B[t * NN + min(j0 + x, NN - 1)];
+        }
+#pragma unroll
+        for (int x = 0; x < BS; ++x)
+#pragma unroll
+          for (int y = 0; y < BS; ++y) acc[x][y] = fma(a[x], b[y], acc[x][y]);
+      }
+#pragma unroll
+      for (int x = 0; x < BS; ++x)
+#pragma unroll
+        for (int y = 0; y < BS; ++y)
+          if (i0 + x < NN && j0 + y < NN) C[(i0 + x) * NN + j0 + y] = acc[x][y];
+    }
+    wave_sync();
+    return;
+  }
   for (int o = lane; o < NN * NN; o += 64) {
     const int i = o / NN, j = o - i * NN;
     double a[NN], b[NN];
