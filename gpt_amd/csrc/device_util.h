@@ -397,17 +397,29 @@ __device__ __forceinline__ void wave_solve(double* M, double* X) {
       wave_sync();
     }
     const double rp = 1.0 / M[c * NN + c];
-    const int rows = NN - c - 1;
-    const int wcols = (NN - c - 1) + NN;
-    for (int o = lane; o < rows * wcols; o += 64) {
-      const int rr = c + 1 + o / wcols, cc = o - (o / wcols) * wcols;
-      const double f = M[rr * NN + c] * rp;
-      if (cc < NN - c - 1) {
-        const int col = c + 1 + cc;
-        M[rr * NN + col] -= f * M[c * NN + col];
-      } else {
-        const int col = cc - (NN - c - 1);
-        X[rr * NN + col] -= f * X[c * NN + col];
+    // lanes over the columns of [M | X] right of the pivot, rows in a uniform loop: the
+    // multiplier M[rr,c]·rp is a broadcast read and no lane divides indices (same arithmetic
+    // per element as a lanes-over-elements sweep)
+    const int mcols = NN - c - 1, wcols = mcols + NN;
+    for (int cc = lane; cc < wcols; cc += 64) {
+      double* colp = cc < mcols ? M + (c + 1 + cc) : X + (cc - mcols);
+      const double piv = colp[c * NN];
+      // rows in blocks of 8, all reads of a block issued before its writes (the column and the
+      // multiplier column never alias, but the compiler cannot know: one row at a time would
+      // serialise on LDS latency)
+      for (int r0 = c + 1; r0 < NN; r0 += 8) {
+        double fv[8], cv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int rr = min(r0 + u, NN - 1);
+          fv[u] = M[rr * NN + c];
+          cv[u] = colp[rr * NN];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double f = fv[u] * rp;
+          if (r0 + u < NN) colp[(r0 + u) * NN] = cv[u] - f * piv;
+        }
       }
     }
     wave_sync();
