@@ -102,10 +102,33 @@ __device__ __forceinline__ double wave_sum(double v) {
   return self_sum<1>(v, lane);
 }
 
+// max(v, partner's v) for the exchange pattern of wave_sum (permlane swaps across 32 / 16, DPP
+// within rows) — no LDS round trip (a __shfl_xor of a double is two ds_bpermute per stage).
+template <int OFF>
+__device__ __forceinline__ double self_max(double v) {
+  if constexpr (OFF == 32 || OFF == 16) {
+    const long long a = __double_as_longlong(v);
+    const unsigned lo = (unsigned)a, hi = (unsigned)(a >> 32);
+    // swapping (v, v): each lane ends up with {own v, partner's v} in its two slots
+    const auto l2 = OFF == 32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                              : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h2 = OFF == 32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                              : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const double x0 = __longlong_as_double(((long long)h2[0] << 32) | (unsigned)l2[0]);
+    const double x1 = __longlong_as_double(((long long)h2[1] << 32) | (unsigned)l2[1]);
+    return fmax(x0, x1);
+  } else {
+    return fmax(v, dpp_partner<OFF>(v));
+  }
+}
+
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-  return v;
+  v = self_max<32>(v);
+  v = self_max<16>(v);
+  v = self_max<8>(v);
+  v = self_max<4>(v);
+  v = self_max<2>(v);
+  return self_max<1>(v);
 }
 
 // Sum of one value per thread over the workgroup; every thread gets the total.
@@ -381,8 +404,22 @@ __device__ __forceinline__ void wave_mm(const double* A, const double* B, double
 
 // Solve M·X = X0 in place (X holds X0 on entry), partial pivoting (LAPACK gesv semantics:
 // largest |pivot|, first index on ties, multipliers scaled by 1/pivot).
+// Large systems (NN >= 16: the 2r x 2r Padé solve at r >= 8) are compiled out of line so the
+// elimination gets its own register allocation instead of the caller's, which at r = 20 is already
+// at the VGPR limit and spilled the block buffers to scratch inside the row loop.
 template <int NN>
-__device__ __forceinline__ void wave_solve(double* M, double* X) {
+__device__ __forceinline__ void wave_solve_body(double* M, double* X, long long* st);
+template <int NN>
+__device__ __noinline__ void wave_solve_ool(double* M, double* X, long long* st) {
+  wave_solve_body<NN>(M, X, st);
+}
+template <int NN>
+__device__ __forceinline__ void wave_solve(double* M, double* X, long long* st = nullptr) {
+  if constexpr (NN >= 16) wave_solve_ool<NN>(M, X, st);
+  else wave_solve_body<NN>(M, X, st);
+}
+template <int NN>
+__device__ __forceinline__ void wave_solve_body(double* M, double* X, long long* st) {
   const int lane = threadIdx.x & 63;
   for (int c = 0; c < NN; ++c) {
     const double mine = (lane >= c && lane < NN) ? fabs(M[lane * NN + c]) : -1.0;
@@ -401,29 +438,38 @@ __device__ __forceinline__ void wave_solve(double* M, double* X) {
     // multiplier M[rr,c]·rp is a broadcast read and no lane divides indices (same arithmetic
     // per element as a lanes-over-elements sweep)
     const int mcols = NN - c - 1, wcols = mcols + NN;
-    for (int cc = lane; cc < wcols; cc += 64) {
-      double* colp = cc < mcols ? M + (c + 1 + cc) : X + (cc - mcols);
-      const double piv = colp[c * NN];
-      // rows in blocks of 8, all reads of a block issued before its writes (the column and the
-      // multiplier column never alias, but the compiler cannot know: one row at a time would
-      // serialise on LDS latency)
+    // a lane owns column cc = lane and, when [M | X] has more than 64 columns right of the pivot,
+    // cc + 64 too; both are updated in the same pass over the rows, which go in blocks of 8 with
+    // all reads of a block issued before its writes (the columns and the multiplier column never
+    // alias, but the compiler cannot know: one row at a time would serialise on LDS latency)
+    if (lane < wcols) {
+      const int cb = lane + 64;
+      const bool two = cb < wcols;
+      double* pa = lane < mcols ? M + (c + 1 + lane) : X + (lane - mcols);
+      double* pb = two ? (cb < mcols ? M + (c + 1 + cb) : X + (cb - mcols)) : pa;
+      const double piva = pa[c * NN], pivb = pb[c * NN];
       for (int r0 = c + 1; r0 < NN; r0 += 8) {
-        double fv[8], cv[8];
+        double fv[8], ca[8], cbv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int rr = min(r0 + u, NN - 1);
           fv[u] = M[rr * NN + c];
-          cv[u] = colp[rr * NN];
+          ca[u] = pa[rr * NN];
+          cbv[u] = pb[rr * NN];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const double f = fv[u] * rp;
-          if (r0 + u < NN) colp[(r0 + u) * NN] = cv[u] - f * piv;
+          if (r0 + u < NN) {
+            pa[(r0 + u) * NN] = ca[u] - f * piva;
+            if (two) pb[(r0 + u) * NN] = cbv[u] - f * pivb;
+          }
         }
       }
     }
     wave_sync();
   }
+  if (st && lane == 0) st[15] = (long long)__builtin_amdgcn_s_memtime();   // diagnostic stamp
   // back substitution: lanes over columns of X; the row of M and the solved rows stay in regs
   for (int col = lane; col < NN; col += 64) {
     double x[NN];
@@ -507,8 +553,14 @@ __device__ __forceinline__ bool wave_solve_dd(const double* M, double* X) {
 // 13th order above, θ13 = 5.4).  Scratch S: 7 NN² doubles; the result is left at S + NN².
 // Returns true if the result contains a NaN (the geod bail-out of GPT_SGLD.jl:23-26).
 template <int NN>
-__device__ bool wave_expm(double* S) {
+__device__ bool wave_expm(double* S, long long* st = nullptr) {
   const int lane = threadIdx.x & 63;
+  // diagnostic stamps (slots 11-14 of the caller's stamp row; grid engine stamp builds only)
+#define GPT_XST(i)                                                        \
+  do {                                                                    \
+    if (st && lane == 0) st[i] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+  GPT_XST(11);
   constexpr int q = NN * NN;
   double* A = S;
   double* A2 = S + q;
@@ -584,6 +636,7 @@ __device__ bool wave_expm(double* S) {
     }
     wave_sync();
   }
+  GPT_XST(12);
   double* M = A4;      // dead from here on
   double* X = A2;
   for (int o = lane; o < q; o += 64) {
@@ -593,12 +646,15 @@ __device__ bool wave_expm(double* S) {
   wave_sync();
   bool solved = false;
   if constexpr (2 * NN <= 64) solved = wave_solve_dd<NN>(M, X);
-  if (!solved) wave_solve<NN>(M, X);
+  if (!solved) wave_solve<NN>(M, X, st);
+  GPT_XST(13);
   for (int z = 0; z < si; ++z) {
     wave_mm<NN>(X, X, T);
     for (int o = lane; o < q; o += 64) X[o] = T[o];
     wave_sync();
   }
+  GPT_XST(14);
+#undef GPT_XST
   bool bad = false;
   for (int o = lane; o < q; o += 64) bad |= (X[o] != X[o]);
   return __any(bad);

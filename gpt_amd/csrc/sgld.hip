@@ -400,7 +400,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
         X0[o] = tt * v;
       }
       wave_sync();
-      const bool bad = wave_expm<2 * R>(X0);
+      const bool bad = wave_expm<2 * R>(
+          X0, P.stamps ? P.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStamps : nullptr);
       for (int o = tid; o < nn * R; o += 64) {
         const int a = o / R, l = o - a * R;
         Ec[o] = X0[nn * nn + a * nn + l];

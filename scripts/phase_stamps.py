@@ -86,6 +86,14 @@ def main():
             print("  %2d %-26s %8.0f cyc  %5.1f%%" % (i, NAMES[i], v, 100 * v / tot))
             prev = i
     print("  total k-block %.0f cycles" % tot)
+    xs = kblocks[..., 11:15]
+    if (xs > 0).all():
+        dx = np.median((xs[..., 1:] - xs[..., :-1]).reshape(-1, 3), axis=0)
+        print("  expm(2r x 2r) inside: products %.0f, solve %.0f, squarings %.0f cycles" % tuple(dx))
+        el = kblocks[..., 15] - kblocks[..., 12]
+        if (kblocks[..., 15] > 0).all():
+            print("  solve: elimination %.0f cycles, back substitution %.0f"
+                  % (np.median(el), np.median(kblocks[..., 13] - kblocks[..., 15])))
     dw = np.median((wblocks[..., 3] - wblocks[..., 0]).ravel())
     print("w-block total %.0f cycles (V-phase %.0f)" % (dw, np.median((wblocks[..., 2] - wblocks[..., 0]).ravel())))
     t_us = s.time_steps(20)
