@@ -421,11 +421,24 @@ __device__ __forceinline__ void wave_solve(double* M, double* X, long long* st =
 template <int NN>
 __device__ __forceinline__ void wave_solve_body(double* M, double* X, long long* st) {
   const int lane = threadIdx.x & 63;
+  // strictly column diagonally dominant M: partial pivoting never swaps (dominance survives
+  // elimination), so the pivot search can be skipped with identical results
+  bool dd = true;
+  if (lane < NN) {
+    double off = 0.0;
+    for (int i = 0; i < NN; ++i)
+      if (i != lane) off += fabs(M[i * NN + lane]);
+    dd = fabs(M[lane * NN + lane]) > off;
+  }
+  const bool nopiv = __all(dd);
   for (int c = 0; c < NN; ++c) {
-    const double mine = (lane >= c && lane < NN) ? fabs(M[lane * NN + c]) : -1.0;
-    const double best = wave_max(mine);
-    const unsigned long long hit = __ballot(mine == best && lane >= c && lane < NN);
-    const int bi = hit ? (int)__ffsll((long long)hit) - 1 : c;
+    int bi = c;
+    if (!nopiv) {
+      const double mine = (lane >= c && lane < NN) ? fabs(M[lane * NN + c]) : -1.0;
+      const double best = wave_max(mine);
+      const unsigned long long hit = __ballot(mine == best && lane >= c && lane < NN);
+      bi = hit ? (int)__ffsll((long long)hit) - 1 : c;
+    }
     if (bi != c) {
       for (int col = lane; col < NN; col += 64) {
         double t0 = M[c * NN + col]; M[c * NN + col] = M[bi * NN + col]; M[bi * NN + col] = t0;
