@@ -107,8 +107,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--chains", type=int, default=0,
-                    help="independent chains per GPU (0: one per CU for the chain engine, "
-                         "CUs // (D+1) for the grid engine, D+1 workgroups per chain)")
+                    help="independent chains per GPU (0: one per CU for the chain engine, two at "
+                         "D <= 4; CUs // (D+1) for the grid engine, D+1 workgroups per chain)")
     ap.add_argument("--engine", default="auto", choices=["auto", "grid", "chain"])
     ap.add_argument("--workload", default="kin40k", choices=sorted(WORKLOADS),
                     help="kin40k (BASELINE configs 3/4, the metric's workload) or powerplant (config 2)")
@@ -172,7 +172,9 @@ def main():
         eng = probe.info()["engine"]
         probe.close()
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        C = cus if eng == "chain" else max(1, cus // (D + 1))   # grid: D+1 workgroups per chain
+        # chain engine: one chain per CU, two at D <= 4 (4-wave build, 80 KB of LDS);
+        # grid engine: D+1 workgroups per chain
+        C = (cus * (2 if D <= 4 else 1)) if eng == "chain" else max(1, cus // (D + 1))
     need = args.warmup + args.steps + args.kernel_steps
     epochs = -(-need // nb) + 1
     seeds = [1000 * rank + c + 1 for c in range(C)]

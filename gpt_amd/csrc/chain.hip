@@ -58,7 +58,7 @@ GPT_HD constexpr int al16c(int x) { return (x + 15) & ~15; }
 // LDS carve of chain_kernel<R, J, G>, fixed at compile time: every table is sized for the
 // engine's maxima (kChainDMax dimensions, Q <= kChainQP, m <= kChainMMax), so every LDS address
 // is a constant and none of them occupies a scalar register (the kernel sits at the SGPR limit).
-template <int R, int G>
+template <int R, int G, int WV = kChainDMax>
 struct ChainLds {
   static constexpr int DRG = kChainDMax * R * G;          // temp entries of a slot
   static constexpr int TS = 2 * (DRG + G);                // temp | ones(G) | 1/temp | ones(G)
@@ -74,9 +74,11 @@ struct ChainLds {
   static constexpr int o_un = al16c(o_misc + 8 * 16);
   // union: w·V rows [row][q] (stride kChainQS) + per-wave reduction scratch (batch loop) |
   // per-wave post-batch scratch
-  static constexpr int L_dbl = G * kChainQS + kChainDMax * G * R * kChainRunS;
+  // (per-wave parts sized for the WV waves of the build: at WV = 4 the carve plus the row staging
+  // stays under 80 KB, two chains per CU)
+  static constexpr int L_dbl = G * kChainQS + WV * G * R * kChainRunS;
   static constexpr int x_dbl = chain_scratch_dbl(R);
-  static constexpr int bytes = al16c(o_un + 8 * (L_dbl > x_dbl * kChainDMax ? L_dbl : x_dbl * kChainDMax));
+  static constexpr int bytes = al16c(o_un + 8 * (L_dbl > x_dbl * WV ? L_dbl : x_dbl * WV));
 };
 
 // Diagnostic phase stamps (gpt_sgld_session_stamps only): s_memtime of wave 0 at phase ends.
@@ -126,18 +128,18 @@ __device__ __forceinline__ void wave_sum_to_lds(double (&v)[2 * NV], double* dst
 // per SIMD leaves the register file to two V tasks per wave even at J = 8 (PowerPlant, D = 4,
 // minibatch 256: 8 tasks per row group).
 template <int R, int J, int G, int WV>
-__global__ __launch_bounds__(64 * WV) void chain_kernel(StepParams P,
+__global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepParams P,
                                                                 const ChainDesc* chains,
                                                                 const long long* __restrict__ tbase,
                                                                 int t_local) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ __attribute__((aligned(16))) double pbuf[kChainBufs * kChainDMax * G * 64 * J];   // row staging
+  __shared__ __attribute__((aligned(16))) double pbuf[kChainBufs * WV * G * 64 * J];   // row staging
   // Chain fields are read through Cp at their point of use (scalar loads) rather than held in
   // SGPRs across the batch loop, where SGPR pressure spills into VGPR lanes.
   const ChainDesc* Cp = chains + blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, k = uni(tid >> 6);
   const int n = P.n, D = P.D, Q = P.Q, m = P.m, NTH = 64 * D;
-  using L = ChainLds<R, G>;
+  using L = ChainLds<R, G, WV>;
   const int NCH = (Q + 63) / 64, NT = NCH * G;                  // q chunks of 64, V tasks
   int* IT_l = (int*)(smem + L::o_IT);
   double* w_l = (double*)(smem + L::o_w);
@@ -666,18 +668,20 @@ __global__ __launch_bounds__(64 * WV) void chain_kernel(StepParams P,
   X(4, 1) X(4, 2) X(4, 4) X(4, 8) X(5, 1) X(5, 2) X(5, 4) X(5, 8)
 
 // Static LDS of chain_kernel<R, J, G>: the row staging buffer.
-static size_t chain_static_lds(int J) { return 8 * (size_t)kChainBufs * kChainDMax * kChainG * 64 * J; }
+static int chain_wv(int D) { return D <= 4 ? 4 : kChainDMax; }
+static size_t chain_static_lds(int J, int WV) { return 8 * (size_t)kChainBufs * WV * kChainG * 64 * J; }
 
 static int chain_J(int n) { return n <= 64 ? 1 : (n <= 128 ? 2 : (n <= 256 ? 4 : (n <= 512 ? 8 : 0))); }
 
 size_t chain_lds_bytes(int n, int D, int r, int Q, int m) {
-  (void)n; (void)D; (void)Q; (void)m;
+  (void)n; (void)Q; (void)m;
+  const bool w4 = chain_wv(D) == 4;
   switch (r) {
-    case 1: return ChainLds<1, kChainG>::bytes;
-    case 2: return ChainLds<2, kChainG>::bytes;
-    case 3: return ChainLds<3, kChainG>::bytes;
-    case 4: return ChainLds<4, kChainG>::bytes;
-    case 5: return ChainLds<5, kChainG>::bytes;
+    case 1: return w4 ? ChainLds<1, kChainG, 4>::bytes : ChainLds<1, kChainG>::bytes;
+    case 2: return w4 ? ChainLds<2, kChainG, 4>::bytes : ChainLds<2, kChainG>::bytes;
+    case 3: return w4 ? ChainLds<3, kChainG, 4>::bytes : ChainLds<3, kChainG>::bytes;
+    case 4: return w4 ? ChainLds<4, kChainG, 4>::bytes : ChainLds<4, kChainG>::bytes;
+    case 5: return w4 ? ChainLds<5, kChainG, 4>::bytes : ChainLds<5, kChainG>::bytes;
     default: return (size_t)1 << 30;
   }
 }
@@ -690,7 +694,7 @@ bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stie
   if (Q > kChainQP || m > kChainMMax) return false;   // the fixed LDS carve's maxima
   const int NT = (Q + 63) / 64 * kChainG;
   if (NT > ((chain_J(n) >= 8 && D > 4) ? 1 : kChainTasks) * D) return false;
-  return chain_lds_bytes(n, D, r, Q, m) + chain_static_lds(chain_J(n)) <= 160 * 1024;
+  return chain_lds_bytes(n, D, r, Q, m) + chain_static_lds(chain_J(n), chain_wv(D)) <= 160 * 1024;
 }
 
 hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchains,
@@ -704,7 +708,7 @@ hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchain
     if (!attr) {                                                                              \
       hipError_t e = hipFuncSetAttribute((const void*)chain_kernel<RR, JJ, kChainG, WW>,      \
                                          hipFuncAttributeMaxDynamicSharedMemorySize,          \
-                                         (int)(160 * 1024 - chain_static_lds(JJ)));           \
+                                         (int)(160 * 1024 - chain_static_lds(JJ, WW)));       \
       if (e != hipSuccess) return e;                                                          \
       attr = true;                                                                            \
     }                                                                                         \
