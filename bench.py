@@ -69,36 +69,94 @@ def algorithmic_flops_per_step(n, D, B, r, Q):
     return 4 * n * r * D * B + 3 * Q * D * B + 4 * Q * B + D * (14 * n * r * r + 2 * 30 * (2 * r) ** 3)
 
 
+def _cpu_threads():
+    """Host threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS is set to it on
+    the GPU box), else every CPU this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:                               # pragma: no cover
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(phi_np, y_np, I, args, seconds):
-    """Oracle (numpy fp64 restatement, single BLAS thread) on the same workload, bounded."""
+    """The C++ fp64 restatement of GPT_SGLD.jl:345-448 (oracle/cpu, test infrastructure) on the
+    same workload, bounded to about ``seconds`` of wall time: 1 chain on 1 core, then T chains on
+    T cores (OpenMP over chains).  Falls back to the numpy oracle (1 core) when the
+    library was not built."""
+    N = phi_np.shape[2]
+    nb = -(-N // args.m)
     try:
-        from threadpoolctl import threadpool_limits
-    except Exception:                                   # pragma: no cover
-        threadpool_limits = None
-    from oracle import gpt_sgld_ref as R
-    ctx = threadpool_limits(limits=1) if threadpool_limits else None
-    try:
-        if ctx:
-            ctx.__enter__()
-        N = phi_np.shape[2]
-        nb = -(-N // args.m)
-        steps, cap = 5, 20000
-        while True:
-            epochs = -(-steps // nb)
-            t0 = time.perf_counter()
-            R.GPTregression(phi_np, y_np, args.signal_var, I, args.r, args.Q, args.m, args.epsw,
-                            args.epsU, 0, epochs, 1, max_steps=steps, store_every=epochs * nb)
-            dt = time.perf_counter() - t0
-            if dt >= 0.8 * seconds or steps >= cap:
-                break
-            steps = min(cap, max(steps + 1, int(steps * seconds / max(dt, 1e-3) * 1.05)))
-    finally:
-        if ctx:
-            ctx.__exit__(None, None, None)
-    return dict(value=steps / dt, unit="SGLD steps/s (1 chain)", cores=1, kind="port",
-                sample="oracle/gpt_sgld_ref.py GPTregression, %d steps of the %s config "
-                       "(n=%d, D=%d, r=%d, Q=%d, m=%d), numpy fp64, 1 BLAS thread, %.1f s incl. init"
-                       % (steps, args.workload, args.n, args.D, args.r, args.Q, args.m, dt))
+        from oracle import cpu_lib
+        cpu_lib.lib()
+    except Exception as exc:                             # pragma: no cover
+        cpu_lib = None
+        why = str(exc)
+    if cpu_lib is None:
+        from oracle import gpt_sgld_ref as R
+        steps = 20
+        t0 = time.perf_counter()
+        R.GPTregression(phi_np, y_np, args.signal_var, I, args.r, args.Q, args.m, args.epsw,
+                        args.epsU, 0, -(-steps // nb), 1, max_steps=steps, store_every=nb)
+        dt = time.perf_counter() - t0
+        return dict(value=steps / dt, unit="SGLD steps/s (1 chain)", cores=1, kind="port",
+                    sample="numpy oracle, %d steps (C++ restatement unavailable: %s)" % (steps, why))
+
+    def run(chains, threads, steps):
+        epochs = -(-steps // nb)
+        o = cpu_lib.GPTregression_chains(phi_np, y_np, args.signal_var, I, args.r, args.Q, args.m,
+                                         args.epsw, args.epsU, 0, epochs,
+                                         [1000 + c for c in range(chains)], threads=threads,
+                                         store_every=epochs * nb, max_steps=steps)
+        return o["steps"] / o["seconds"], o["steps"], o["seconds"]
+
+    probe, _, _ = run(1, 1, 20)
+    s1 = max(20, int(probe * 0.3 * seconds))
+    one, st1, dt1 = run(1, 1, s1)
+    T = _cpu_threads()
+    sT = max(10, int(one * 0.6 * seconds))               # per chain: ~0.6·seconds if T cores scale
+    allc, stT, dtT = run(T, T, sT)
+    return dict(value=allc, unit="chain-steps/s (%d chains on %d cores)" % (T, T), cores=T,
+                kind="port", single_core_steps_per_s=one, nproc=os.cpu_count(),
+                cpu_model=cpu_lib.cpu_model(),
+                sample="oracle/cpu/gpt_sgld_cpu.cpp (C++ fp64 restatement of GPT_SGLD.jl:345-448, "
+                       "OpenMP over chains, no BLAS) on the %s config (n=%d, D=%d, r=%d, Q=%d, m=%d): "
+                       "1 chain x %d steps on 1 core in %.1f s; %d chains x %d steps on %d cores in "
+                       "%.1f s" % (args.workload, args.n, args.D, args.r, args.Q, args.m, st1, dt1,
+                                   T, sT, T, dtT))
+
+
+def launch_command(argv, nproc, port, script=None):
+    """The torchrun command bench.py re-runs itself under for --gpus N > 1 (one rank per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            "--nproc-per-node", str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(script or __file__)] + list(argv)
+
+
+def self_launch(argv, nproc, script=None):
+    """Start N ranks as a child torchrun and return its exit code.  Called before anything in
+    this process touches the GPU (no exec: a child process)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launch_command(argv, nproc, port, script), env=env)
+
+
+def max_over_ranks(dt, device=None):
+    """Slowest rank's wall time (the timed region's value is whole-job work over this)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return dt
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def main():
@@ -125,11 +183,19 @@ def main():
     ap.add_argument("--signal_var", type=float, default=None, help="default: the workload's")
     ap.add_argument("--kernel-steps", type=int, default=100, help="steps of the event-timed pass")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--epochs", type=int, default=200,
+                    help="epochs every chain runs in total (kin40kExperiment.jl:74: maxepoch 200); "
+                         "the steps after the timed region finish them for the converged test RMSE")
+    ap.add_argument("--last-epochs", type=int, default=50,
+                    help="epoch-end samples per chain in the posterior mean (kin40kExperiment.jl:80-87)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single-chain", dest="single_chain", action="store_false",
                     help="skip the C=1 latency pass (one chain on one CU)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: re-run under torchrun before any HIP call in this process
+        raise SystemExit(self_launch(sys.argv[1:], args.gpus))
     loader, wD, wm, wls, sigma_rbf, wsv, wdesc = WORKLOADS[args.workload]
     if args.D is None:
         args.D = wD
@@ -167,21 +233,36 @@ def main():
     nb = -(-N // m)
     C = args.chains
     if C <= 0:
-        probe = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0, 1,
-                            [1], store=False, engine=args.engine)
-        eng = probe.info()["engine"]
-        probe.close()
+        # filling the GPU: the chain engine whenever it takes the shape (one chain's session
+        # would pick the grid engine, the single-chain latency choice)
+        eng = "grid"
+        if args.engine in ("auto", "chain"):
+            from gpt_amd._lib import GPTError
+            try:
+                probe = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU,
+                                    args.signal_var, 0, 1, [1], store=False, engine="chain")
+                eng = "chain"
+                probe.close()
+            except GPTError:
+                if args.engine == "chain":
+                    raise
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         # chain engine: one chain per CU, two at D <= 4 (4-wave build, 80 KB of LDS);
         # grid engine: D+1 workgroups per chain
         C = (cus * (2 if D <= 4 else 1)) if eng == "chain" else max(1, cus // (D + 1))
     need = args.warmup + args.steps + args.kernel_steps
     epochs = -(-need // nb) + 1
+    epochs_total = max(args.epochs, epochs)
+    last = max(1, min(args.last_epochs, epochs_total))
     seeds = [1000 * rank + c + 1 for c in range(C)]
-    sess = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0, epochs,
-                       seeds, store_every=nb, store=True, engine=args.engine)
+    # burn-in = all but the last `last` epochs: the timed steps store nothing, the epoch-end
+    # samples of the last epochs feed the converged posterior mean
+    sess = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var,
+                       epochs_total - last, last, seeds, store_every=nb, store=True,
+                       engine=args.engine)
     info = sess.info()
     sess.run(args.warmup)
+    sess.prepare(args.steps)           # capture the timed steps' graphs outside the timed region
     sess.sync()
     if world > 1:
         dist.barrier()
@@ -192,11 +273,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dt = float(tmax.item())
+    dt = max_over_ranks(time.perf_counter() - t0, dev)
     total_steps = C * args.steps * world
     value = total_steps / dt
     ms_per_step = 1000.0 * dt / args.steps
@@ -210,18 +287,54 @@ def main():
     B = m
     bytes_launch = C * algorithmic_bytes_per_step(n, D, B, r, Q)
     achieved = bytes_launch / (k_us * 1e-6) / 1e9
-    traffic = None
+    # HBM traffic per launch is a PMC quantity (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950
+    # FETCH doubling): it cannot be read inside this run, so it comes from the stored profile of
+    # the same shape, with its tag (scripts/pmc_chain.sh -> profiles/pmc_traffic.json)
+    traffic, traffic_src = None, None
     if os.path.exists(args.pmc):
         try:
             pm = json.load(open(args.pmc))
             key = "C%d_n%d_D%d_r%d_Q%d_m%d" % (C, n, D, r, Q, m)
-            traffic = pm.get(key, {}).get("hbm_bytes_per_launch")
+            ent = pm.get(key, {})
+            traffic = ent.get("hbm_bytes_per_launch")
+            if traffic is not None:
+                traffic_src = "stored PMC profile %s[%s] (%s)" % (
+                    os.path.relpath(args.pmc, ROOT), key, ent.get("source", "untagged"))
         except Exception:
             traffic = None
 
+    # ---- quality leg (the metric's "+ test RMSE"): every chain finishes its epochs_total epochs
+    # (kin40kExperiment.jl:74) and the ensemble prediction is the mean over every chain's last
+    # `last` epoch-end samples (:80-87), all-reduced over ranks (RCCL, config 4)
+    from gpt_amd.ensemble import combine_predictive_mean, rmse as ens_rmse
+    I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
+    tq = time.perf_counter()
+    sess.run(sess.total_steps)
+    sess.sync()
+    quality_train_s = time.perf_counter() - tq
+    status = [sess.fetch(c)[2] for c in range(C)]
+    fsum_q = torch.zeros(Nte, dtype=torch.float64, device=dev)
+    cnt = 0
+    fhq = torch.empty((last, Nte), dtype=torch.float64, device=dev)
+    for c in range(C):
+        if status[c] != 0:
+            continue
+        _, _, ws, Us, ns = sess.device_state(c)
+        pred_device(ws, Us, I0, phi_te, n, D, Nte, r, Q, ns, fhq)
+        fsum_q += fhq[:ns].sum(dim=0)
+        cnt += ns
+    torch.cuda.synchronize()
+    fmean_q = combine_predictive_mean(fsum_q, cnt)
+    rmse_conv = ens_rmse(yte, fmean_q.cpu().numpy(), ysd)
+    quality = {"test_rmse": rmse_conv, "epochs": epochs_total, "samples_per_chain": last,
+               "chains": C * world, "bailed_out": int(sum(1 for x in status if x != 0)),
+               "train_s": quality_train_s,
+               "note": "RMSE (original units, ytrainStd x) of the mean prediction over the last %d "
+                       "epoch-end samples of every chain after %d epochs (kin40kExperiment.jl:74-87)"
+                       % (last, epochs_total)}
+
     # posterior predictive over every chain's final state as ONE stacked-sample prediction
     # (fp64-MFMA phidotU GEMM with M = S·r, N = Ntest, K = n per dimension, then the V-phase)
-    I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
     npred = C
     w_all = torch.empty((npred, Q), dtype=torch.float64, device=dev)
     U_all = torch.empty((npred, n * r * D), dtype=torch.float64, device=dev)
@@ -238,22 +351,27 @@ def main():
     pred_ms = ev0.elapsed_time(ev1)
     pred_flop = 2.0 * npred * r * n * D * Nte             # the GEMM (dominant); V-phase excluded
     fsum = fh.sum(dim=0)
-    from gpt_amd.ensemble import combine_predictive_mean, rmse as ens_rmse
     combine_predictive_mean(torch.zeros_like(fsum), 1)   # warm-up (communicator setup, kernels)
     torch.cuda.synchronize()
     ta = time.perf_counter()
     fmean = combine_predictive_mean(fsum, npred)     # RCCL all-reduce across ranks (config 4)
     torch.cuda.synchronize()
     allreduce_ms = 1000.0 * (time.perf_counter() - ta)
-    rmse = ens_rmse(yte, fmean.cpu().numpy(), ysd)
+    rmse_final = ens_rmse(yte, fmean.cpu().numpy(), ysd)
 
     single = None
     if args.single_chain and rank == 0:
         s1 = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0,
                          epochs, [7], store_every=nb, store=False, engine=args.engine)
-        s1.run(args.warmup); s1.sync()
+        s1.run(args.warmup)
+        s1.prepare(args.steps)
+        s1.sync()
         t1 = time.perf_counter(); s1.run(args.steps); s1.sync()
-        single = args.steps / (time.perf_counter() - t1)
+        sps = args.steps / (time.perf_counter() - t1)
+        s1_us = s1.time_steps(min(args.kernel_steps, s1.total_steps - s1.steps_done))
+        b1 = algorithmic_bytes_per_step(n, D, m, r, Q)
+        single = {"steps_per_s": sps, "engine": s1.info()["engine"], "kernel_us": s1_us,
+                  "roofline_frac": (b1 / (s1_us * 1e-6) / 1e9 / HBM_PEAK_GBS) if s1_us else None}
         s1.close()
 
     cpu = None
@@ -268,6 +386,7 @@ def main():
             "value": value,
             "unit": "chain-steps/s",
             "n_gpus": world,
+            "world_size_seen": (dist.get_world_size() if world > 1 else 1),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
@@ -285,21 +404,24 @@ def main():
                        "threads_per_workgroup": info["threads"], "lds_bytes": info["lds_bytes"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": ("chain_kernel<%d,J,2>" if info["engine"] == "chain"
                                     else "sgld_step_kernel<%d>") % r, "kernel_us": k_us,
                          "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
-            "test_rmse": rmse,
-            "test_rmse_note": "ensemble of %d chains x %d ranks after %d steps/chain (%.1f epochs)"
-                              % (npred, world, args.warmup + args.steps, (args.warmup + args.steps) / nb),
+            "test_rmse": quality["test_rmse"],
+            "test_rmse_note": quality["note"],
+            "quality": quality,
             "allreduce_ms": allreduce_ms,
             "pred": {"samples": npred, "Ntest": Nte, "ms": pred_ms, "gemm_flop": pred_flop,
                      "achieved_tflops": pred_flop / (pred_ms * 1e-3) / 1e12,
                      "peak_tflops": FP64_MFMA_PEAK_TFS,
                      "frac": pred_flop / (pred_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS,
                      "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + pred_vphase_kernel",
-                     "note": "whole stacked-sample call timed with events (GEMM + V-phase)"},
-            "single_chain_steps_per_s": single,
+                     "note": "whole stacked-sample call timed with events (GEMM + V-phase)",
+                     "final_state_ensemble_rmse": rmse_final},
+            "single_chain": single,
+            "single_chain_steps_per_s": single["steps_per_s"] if single else None,
         }
         print(json.dumps(out))
     sess.close()

@@ -5,7 +5,7 @@ Same function names, argument meaning, return values and error behaviour as the 
 
     feature(X, length_scale, sigma_RBF, phi_scale, Z, b)      GPT_SGLD.jl:71    (Gen D)
     feature(X, n, length_scale, sigma_RBF, seed, scale)       kin40kExperiment.jl:71 (Gen C)
-    feature(X, n, length_scale, seed)                         GPT_SGLD_p.jl:40  (Gen A)
+    feature(X, n, length_scale, seed)                         GPT_SGLD_p.jl:40  (Gen A: b=randn)
     featureNotensor(X, length_scale, sigma_RBF, Z, b)         GPT_SGLD.jl:109   (Gen D)
     featureNotensor(X, n, length_scale, sigma_RBF, seed)      PowerPlantNoTensorExperiment.jl:32
     samplenz(r, D, Q, seed)                                   GPT_SGLD_p.jl:57
@@ -68,6 +68,22 @@ def feature_inputs(n, D, seed):
     return Z, b
 
 
+def feature_inputs_a(n, D, seed):
+    """Seeded Generation-A inputs (GPT_SGLD_p.jl:40-54): ``Z = randn(n,D)``, ``b = randn(n,D)``."""
+    Z = np.empty((n, D), order="F")
+    b = np.empty((n, D), order="F")
+    check(lib().gpt_feature_inputs_a(n, D, int(seed) & (2 ** 64 - 1), _ptr(Z), _ptr(b)))
+    return Z, b
+
+
+def epoch_orders(N, seed, epochs):
+    """Row order of every epoch of a chain with ``param_seed`` = seed (randperm + phi[:,:,perm],
+    GPT_SGLD.jl:373-374), built on the device: (N, epochs) int32, 0-based."""
+    out = np.empty((int(N), int(epochs)), dtype=np.int32, order="F")
+    check(lib().gpt_epoch_orders(int(N), int(seed) & (2 ** 64 - 1), int(epochs), _ptr(out, P_I32)))
+    return out
+
+
 def _feature_D(X, length_scale, sigma_RBF, phi_scale, Z, b):
     X = _f64(X)
     N, D = X.shape
@@ -98,9 +114,14 @@ def feature(X, *args):
         Z, b = feature_inputs(int(n), np.shape(X)[1], seed)
         return _feature_D(X, ls, 1.0, scale, Z, b)
     if len(args) == 3:                                    # Gen A: n, ls, seed
+        # GPT_SGLD_p.jl:40-54: Z = randn(n,D)/length_scale, b = randn(n,D), phi = sqrt(2/n)·
+        # cos(X[i,k]·Z[j,k] + b[j,k]) — no sigma_RBF / scale; Z/ℓ is formed first as there (the
+        # kernel's argument X·Z'/1 is then the same double)
         n, ls, seed = args
-        Z, b = feature_inputs(int(n), np.shape(X)[1], seed)
-        return _feature_D(X, ls, 1.0, 1.0, Z, b)
+        if np.size(ls) != 1:
+            raise TypeError("feature(X,n,length_scale,seed): length_scale is a scalar (GPT_SGLD_p.jl:40)")
+        Z, b = feature_inputs_a(int(n), np.shape(X)[1], seed)
+        return _feature_D(X, 1.0, 1.0, 1.0, Z / float(np.ravel(ls)[0]), b)
     raise TypeError("feature: unsupported argument list")
 
 

@@ -37,6 +37,8 @@ SIGNATURES = {
     "gpt_feature_notensor": (C.c_int, [P_D, C.c_int64, C.c_int64, P_D, C.c_int64, C.c_double,
                                        P_D, P_D, C.c_int64, P_D]),
     "gpt_feature_inputs": (C.c_int, [C.c_int64, C.c_int64, C.c_uint64, P_D, P_D]),
+    "gpt_feature_inputs_a": (C.c_int, [C.c_int64, C.c_int64, C.c_uint64, P_D, P_D]),
+    "gpt_epoch_orders": (C.c_int, [C.c_int64, C.c_uint64, C.c_int64, P_I32]),
     "gpt_samplenz": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.c_uint64, P_I32]),
     "gpt_sgld_init": (C.c_int, [C.POINTER(SGLDConfig), P_D, P_D]),
     "gpt_sgld_regression": (C.c_int, [C.POINTER(SGLDConfig), P_D, P_D, P_I32, P_D, P_D, P_D, P_D,
@@ -45,6 +47,7 @@ SIGNATURES = {
                                           C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), P_I32,
                                           C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]),
     "gpt_sgld_session_run": (C.c_int, [C.c_void_p, C.c_int64]),
+    "gpt_sgld_session_prepare": (C.c_int, [C.c_void_p, C.c_int64]),
     "gpt_sgld_session_set_rmsprop": (C.c_int, [C.c_void_p, C.c_double, C.c_double]),
     "gpt_sgld_rmsprop": (C.c_int, [C.POINTER(SGLDConfig), C.c_double, C.c_double, P_D, P_D, P_I32,
                                    P_D, P_D, P_D, P_D, P_D]),

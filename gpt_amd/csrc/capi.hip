@@ -128,8 +128,9 @@ void host_init_state(int n, int r, int D, int Q, uint64_t seed, bool stiefel, do
   }
 }
 
-// Cumulative epoch orders: phi=phi[:,:,perm] every epoch composes the permutations
-// (GPT_SGLD.jl:373-374); order_e = order_{e-1}[perm_e], perm_e Fisher–Yates on PERM stream.
+// Cumulative epoch orders on the host (GPNT_SGLD only; sessions build them on the device, order.hip):
+// phi=phi[:,:,perm] every epoch composes the permutations (GPT_SGLD.jl:373-374);
+// order_e = order_{e-1}[perm_e], perm_e Fisher–Yates on the PERM stream.
 void host_epoch_orders(int N, uint64_t seed, int epochs, int32_t* out) {
   std::vector<int32_t> cur(N), p(N);
   for (int i = 0; i < N; ++i) cur[i] = i;
@@ -198,9 +199,14 @@ struct gpt_sgld_session {
   std::vector<std::unique_ptr<DevMem>> chain_mem;
   std::vector<ChainDesc> chains_h;
   bool temp_ready = false;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t gexec = nullptr;
-  int graph_steps = 0;
+  // Captured step sequences, keyed by where they start in an epoch (b0 = first step % numbatches,
+  // which fixes where the epoch-order builds sit) and their length.  A replay reads the step
+  // counter from the device, so one graph serves every epoch.
+  struct GraphEnt { long long b0; int len; hipGraph_t g; hipGraphExec_t x; };
+  std::vector<GraphEnt> graphs;
+  bool ran = false;                   // a step has been enqueued (RMSprop must be set before)
+  int graph_steps = 0;                // canonical chunk: one epoch (<= 512 steps)
+  DevMem ord_ws;                      // epoch-order workspace when a shuffle exceeds LDS
   bool store = false, diag = false;
   int engine = 0;                     // kEngineGrid / kEngineChain
   DevMem runq;
@@ -208,8 +214,11 @@ struct gpt_sgld_session {
 
 // Engine choice: store_flags bit 2 (or bit 4, w-only steps) forces the grid engine (sgld.hip), bit 3 the chain engine
 // (chain.hip); otherwise GPTSGLD_ENGINE=grid|chain, otherwise chain whenever it supports the shape.
+// Without a forced choice, few chains go to the grid engine (D+1 workgroups per chain: the shorter
+// step) as long as every chain's workgroups fit the GPU at once; more chains go to the chain engine
+// (one workgroup per chain, one batch read per step: the higher throughput).
 static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t flags,
-                       int* engine) {
+                       int nchains, int* engine) {
   int max_run = 0;                    // longest run of core entries sharing one I[·,k] value
   for (int k = 0; k < (int)c->D; ++k) {
     std::vector<int> cnt((size_t)c->r + 1, 0);
@@ -233,6 +242,13 @@ static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t 
   }
   if (want == kEngineGrid && !grid_ok) {
     set_error("grid engine: working set exceeds 160 KiB LDS"); return GPT_ERR_BAD_DIMS;
+  }
+  if (want < 0 && chain_ok && grid_ok) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        (long long)nchains * (c->D + 1) <= cus)
+      want = kEngineGrid;
   }
   *engine = want >= 0 ? want : (chain_ok ? kEngineChain : kEngineGrid);
   return GPT_OK;
@@ -292,9 +308,22 @@ static int session_prime(gpt_sgld_session* s) {
   return GPT_OK;
 }
 
+// Before the first step of epoch e, order_{e+1} goes into the ring slot order_{e-1} leaves
+// (order.hip).  t_host = the step's index as the host counts it: in a captured sequence only its
+// position in the epoch matters (the kernel reads the step counter from the device).
+static hipError_t session_epoch_order(gpt_sgld_session* s, long long t_host, int t_local) {
+  if (t_host % s->P.nb != 0) return hipSuccess;
+  return launch_epoch_order(s->chains_d.as<ChainDesc>(), s->nchains, s->P.N, s->P.nb,
+                            s->total_steps, s->tbase.as<long long>(), t_local, -1,
+                            s->ord_ws.as<int32_t>(), s->stream);
+}
+
 static int session_enqueue(gpt_sgld_session* s, int count) {
+  s->ran = true;
   for (int i = 0; i < count; ++i) {
-    hipError_t e = session_launch(s, s->P, i);
+    hipError_t e = session_epoch_order(s, s->steps_done + i, i);
+    if (e != hipSuccess) return hip_fail(e, "launch_epoch_order");
+    e = session_launch(s, s->P, i);
     if (e != hipSuccess) return hip_fail(e, "launch_step");
   }
   hipError_t e = launch_advance(s->tbase.as<long long>(), count, s->stream);
@@ -322,7 +351,7 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
 
   std::unique_ptr<gpt_sgld_session> s(new gpt_sgld_session());
   {
-    const int rc = pick_engine(cfg, I_host, store_flags, &s->engine);
+    const int rc = pick_engine(cfg, I_host, store_flags, nchains, &s->engine);
     if (rc != GPT_OK) return rc;
   }
   s->cfg = *cfg;
@@ -372,12 +401,11 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   auto up = [](size_t x) { return (x + a - 1) / a * a; };
   const size_t b_w = up(8 * 2 * (size_t)Q), b_U = up(8 * (size_t)n * r * D),
                b_temp = up(8 * 2 * (size_t)D * r * m),
-               b_ord = up(4 * (size_t)s->epochs * N),
+               b_ord = up(4 * 2 * (size_t)N),
                b_ws = s->store ? up(8 * (size_t)Q * s->nstore) : 0,
                b_Us = s->store ? up(8 * (size_t)n * r * D * s->nstore) : 0,
                b_dg = s->diag ? up(8 * (size_t)(1 + D) * s->total_steps) : 0;
   std::vector<double> w0(Q), U0((size_t)n * r * D);
-  std::vector<int32_t> ord((size_t)s->epochs * N);
   s->chains_h.resize(nchains);
   for (int c = 0; c < nchains; ++c) {
     std::unique_ptr<DevMem> mem(new DevMem());
@@ -389,7 +417,7 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     C.w = (double*)base;
     C.U = (double*)(base + b_w);
     C.temp = (double*)(base + b_w + b_U);
-    C.order = (const int32_t*)(base + b_w + b_U + b_temp);
+    C.order = (int32_t*)(base + b_w + b_U + b_temp);
     C.w_store = s->store ? (double*)(base + b_w + b_U + b_temp + b_ord) : nullptr;
     C.U_store = s->store ? (double*)(base + b_w + b_U + b_temp + b_ord + b_ws) : nullptr;
     C.diag = s->diag ? (double*)(base + b_w + b_U + b_temp + b_ord + b_ws + b_Us) : nullptr;
@@ -398,10 +426,8 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     C.gw = C.gU = C.res = nullptr;
     C.epsw = cfg->epsw; C.epsU = cfg->epsU; C.signal_var = cfg->signal_var; C.sigma_w = cfg->sigma_w;
     host_init_state(n, r, D, Q, seeds[c], cfg->stiefel != 0, cfg->sigma_w, w0.data(), U0.data());
-    host_epoch_orders(N, seeds[c], s->epochs, ord.data());
     HIPCHK(hipMemcpy(C.w, w0.data(), 8 * (size_t)Q, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(C.U, U0.data(), 8 * U0.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy((void*)C.order, ord.data(), 4 * ord.size(), hipMemcpyHostToDevice));
     if (s->store) HIPCHK(hipMemset(C.w_store, 0, b_ws + b_Us));
     if (s->diag) HIPCHK(hipMemset(C.diag, 0, b_dg));
     s->chain_mem.push_back(std::move(mem));
@@ -409,6 +435,11 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   HIPCHK(s->chains_d.alloc(sizeof(ChainDesc) * nchains));
   HIPCHK(hipMemcpy(s->chains_d.p, s->chains_h.data(), sizeof(ChainDesc) * nchains,
                    hipMemcpyHostToDevice));
+  // order_0 of every chain (the first step builds order_1, session_epoch_order)
+  if (const size_t wsi = epoch_order_ws_ints(N, nchains)) HIPCHK(s->ord_ws.alloc(4 * wsi));
+  HIPCHK(launch_epoch_order(s->chains_d.as<ChainDesc>(), nchains, N, (int)s->numbatches,
+                            s->total_steps, s->tbase.as<long long>(), 0, 0, s->ord_ws.as<int32_t>(),
+                            s->stream));
   s->graph_steps = (int)std::min<long long>(std::max<long long>(s->numbatches, 1), 512);
   *out = s.release();
   return GPT_OK;
@@ -462,7 +493,7 @@ extern "C" int gpt_sgld_session_set_rmsprop(gpt_sgld_session* s, double epsilon,
     set_error("GPT_SGLDERM_RMSprop is the SGLD + Stiefel sampler (langevin = stiefel = 1)");
     return GPT_ERR_BAD_DIMS;
   }
-  if (s->steps_done != 0 || s->gexec) { set_error("set RMSprop before the first run"); return GPT_ERR_BAD_DIMS; }
+  if (s->steps_done != 0 || s->ran) { set_error("set RMSprop before the first run"); return GPT_ERR_BAD_DIMS; }
   if (!(epsilon > 0) || !(alpha >= 0 && alpha < 1)) {
     set_error("RMSprop needs epsilon > 0 and 0 <= alpha < 1"); return GPT_ERR_BAD_DIMS;
   }
@@ -470,6 +501,37 @@ extern "C" int gpt_sgld_session_set_rmsprop(gpt_sgld_session* s, double epsilon,
   if (rc != GPT_OK) return rc;
   s->P.rms = 1; s->P.rms_eps = epsilon; s->P.rms_alpha = alpha;
   return GPT_OK;
+}
+
+// The graph replaying `len` steps from a start at b0 = step % numbatches (captured on first use).
+static int session_graph(gpt_sgld_session* s, int len, hipGraphExec_t* out) {
+  const long long b0 = s->steps_done % s->P.nb;
+  for (auto& g : s->graphs)
+    if (g.b0 == b0 && g.len == len) { *out = g.x; return GPT_OK; }
+  if (s->graphs.size() >= 16) {                // bounded cache: drop the oldest
+    (void)hipGraphExecDestroy(s->graphs.front().x);
+    (void)hipGraphDestroy(s->graphs.front().g);
+    s->graphs.erase(s->graphs.begin());
+  }
+  HIPCHK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+  int rc = session_enqueue(s, len);
+  hipGraph_t g = nullptr;
+  hipError_t ee = hipStreamEndCapture(s->stream, &g);
+  if (rc != GPT_OK) { if (g) (void)hipGraphDestroy(g); return rc; }
+  if (ee != hipSuccess) return hip_fail(ee, "hipStreamEndCapture");
+  hipGraphExec_t x = nullptr;
+  ee = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+  if (ee != hipSuccess) { (void)hipGraphDestroy(g); return hip_fail(ee, "hipGraphInstantiate"); }
+  s->graphs.push_back({b0, len, g, x});
+  *out = x;
+  return GPT_OK;
+}
+
+// Chunks of a run of n steps from the current step: up to the end of the current epoch, then whole
+// epochs (graph_steps), then the remainder.
+static int session_next_chunk(const gpt_sgld_session* s, long long remaining, long long at) {
+  const long long to_epoch_end = s->graph_steps - (at % s->P.nb) % s->graph_steps;
+  return (int)std::min<long long>(remaining, to_epoch_end);
 }
 
 extern "C" int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps) {
@@ -481,27 +543,44 @@ extern "C" int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps) {
     if (rc != GPT_OK) return rc;
   }
   while (remaining > 0) {
-    const int chunk = (int)std::min<long long>(remaining, s->graph_steps);
-    if (chunk == s->graph_steps) {
-      if (!s->gexec) {
-        HIPCHK(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
-        int rc = session_enqueue(s, chunk);
-        hipGraph_t g = nullptr;
-        hipError_t ee = hipStreamEndCapture(s->stream, &g);
-        if (rc != GPT_OK) return rc;
-        if (ee != hipSuccess) return hip_fail(ee, "hipStreamEndCapture");
-        s->graph = g;
-        HIPCHK(hipGraphInstantiate(&s->gexec, s->graph, nullptr, nullptr, 0));
-      }
-      HIPCHK(hipGraphLaunch(s->gexec, s->stream));
+    const int chunk = session_next_chunk(s, remaining, s->steps_done);
+    // a whole canonical chunk, or any chunk prepared beforehand (gpt_sgld_session_prepare), runs as
+    // one graph; other partial chunks are launched directly
+    const long long b0 = s->steps_done % s->P.nb;
+    bool cached = false;
+    for (auto& g : s->graphs) cached |= (g.b0 == b0 && g.len == chunk);
+    if (chunk == s->graph_steps || cached) {
+      hipGraphExec_t x = nullptr;
+      const int rc = session_graph(s, chunk, &x);
+      if (rc != GPT_OK) return rc;
+      HIPCHK(hipGraphLaunch(x, s->stream));
+      s->ran = true;
     } else {
-      int rc = session_enqueue(s, chunk);
+      const int rc = session_enqueue(s, chunk);
       if (rc != GPT_OK) return rc;
     }
     s->steps_done += chunk;
     remaining -= chunk;
   }
   return GPT_OK;
+}
+
+extern "C" int gpt_sgld_session_prepare(gpt_sgld_session* s, int64_t nsteps) {
+  if (!s) { set_error("null session"); return GPT_ERR_BAD_DIMS; }
+  long long remaining = std::min<long long>(nsteps, s->total_steps - s->steps_done);
+  const long long saved = s->steps_done;
+  const bool ran = s->ran;
+  int rc = GPT_OK;
+  while (remaining > 0 && rc == GPT_OK) {  // the same chunking as gpt_sgld_session_run
+    const int chunk = session_next_chunk(s, remaining, s->steps_done);
+    hipGraphExec_t x = nullptr;
+    rc = session_graph(s, chunk, &x);
+    s->steps_done += chunk;
+    remaining -= chunk;
+  }
+  s->steps_done = saved;                   // capture enqueues nothing: the position is unchanged
+  s->ran = ran;
+  return rc;
 }
 
 extern "C" int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, double* avg_us) {
@@ -516,7 +595,10 @@ extern "C" int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, 
   std::vector<hipEvent_t> ev(2 * cnt, nullptr);
   for (auto& e : ev) HIPCHK(hipEventCreate(&e));
   int rc = GPT_OK;
+  s->ran = true;
   for (long long i = 0; i < cnt && rc == GPT_OK; ++i) {
+    hipError_t eo = session_epoch_order(s, s->steps_done + i, (int)i);   // outside the event pair
+    if (eo != hipSuccess) return hip_fail(eo, "launch_epoch_order");
     HIPCHK(hipEventRecord(ev[2 * i], s->stream));
     hipError_t e = session_launch(s, s->P, (int)i);
     if (e != hipSuccess) rc = hip_fail(e, "launch_step");
@@ -553,8 +635,11 @@ extern "C" int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int6
   HIPCHK(buf.alloc(8 * per * cnt));
   HIPCHK(hipMemset(buf.p, 0, 8 * per * cnt));
   StepParams P = s->P;
+  s->ran = true;
   for (long long i = 0; i < cnt; ++i) {
     P.stamps = buf.as<long long>() + per * i;
+    hipError_t eo = session_epoch_order(s, s->steps_done + i, (int)i);
+    if (eo != hipSuccess) return hip_fail(eo, "launch_epoch_order");
     hipError_t e = session_launch(s, P, (int)i);
     if (e != hipSuccess) return hip_fail(e, "launch_step");
   }
@@ -648,8 +733,10 @@ extern "C" int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double
 extern "C" void gpt_sgld_session_destroy(gpt_sgld_session* s) {
   if (!s) return;
   (void)hipStreamSynchronize(s->stream);
-  if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
-  if (s->graph) (void)hipGraphDestroy(s->graph);
+  for (auto& g : s->graphs) {
+    (void)hipGraphExecDestroy(g.x);
+    (void)hipGraphDestroy(g.g);
+  }
   if (s->own_stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -839,6 +926,40 @@ extern "C" int gpt_feature_inputs(int64_t n, int64_t D, uint64_t seed, double* Z
       const U4 x = philox4x32((uint32_t)e, 0, kFeatB, 0, seed);
       b_out[e] = 2.0 * 3.141592653589793 * u53(x.x, x.y);
     }
+  }
+  return GPT_OK;
+}
+
+// Generation-A feature inputs (GPT_SGLD_p.jl:40-54): Z = randn(n,D) (the Gen-C Z stream) and
+// b = randn(n,D) on the FEAT_B stream with c3 = 1 (Gen C draws b = 2π·rand on c3 = 0).
+extern "C" int gpt_feature_inputs_a(int64_t n, int64_t D, uint64_t seed, double* Z_out, double* b_out) {
+  if (n < 1 || D < 1) { set_error("bad dims"); return GPT_ERR_BAD_DIMS; }
+  for (int64_t e = 0; e < n * D; ++e) {
+    if (Z_out) Z_out[e] = host_normal(seed, (uint32_t)e, 0, kFeatZ, 0);
+    if (b_out) b_out[e] = host_normal(seed, (uint32_t)e, 0, kFeatB, 1);
+  }
+  return GPT_OK;
+}
+
+// randperm(N) + phi = phi[:,:,perm] (GPT_SGLD.jl:373-374) for `epochs` epochs, built on the device
+// by the sampler's own kernel (order.hip).  out: (N, epochs) column-major, 0-based rows.
+extern "C" int gpt_epoch_orders(int64_t N, uint64_t seed, int64_t epochs, int32_t* out) {
+  if (N < 1 || N > (1LL << 31) - 1 || epochs < 0 || epochs > (1 << 20) || (epochs && !out)) {
+    set_error("bad epoch-order arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  DevMem ring, cd, ws;
+  HIPCHK(ring.alloc(8 * (size_t)N));
+  ChainDesc C{};
+  C.order = ring.as<int32_t>();
+  C.seed = seed;
+  HIPCHK(cd.alloc(sizeof(ChainDesc)));
+  HIPCHK(hipMemcpy(cd.p, &C, sizeof(ChainDesc), hipMemcpyHostToDevice));
+  if (const size_t wsi = epoch_order_ws_ints((int)N, 1)) HIPCHK(ws.alloc(4 * wsi));
+  for (int64_t e = 0; e < epochs; ++e) {
+    HIPCHK(launch_epoch_order(cd.as<ChainDesc>(), 1, (int)N, 1, 0, nullptr, 0, (int)e,
+                              ws.as<int32_t>(), nullptr));
+    HIPCHK(hipMemcpy(out + (size_t)e * N, ring.as<int32_t>() + (size_t)(e & 1) * N, 4 * (size_t)N,
+                     hipMemcpyDeviceToHost));
   }
   return GPT_OK;
 }

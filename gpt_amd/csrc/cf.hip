@@ -192,7 +192,9 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
   double* er = tV + (size_t)m * R;              // m       rating, then residual
   int* us = (int*)(er + m);                     // m
   int* ms = us + m;                             // m
-  double* scr = (double*)(ms + m);              // Stiefel scratch (2m ints keep 8-B alignment)
+  // Stiefel scratch of the U / V moves: aliases the batch buffers (sU .. ms), which are dead from
+  // the barrier before the moves until the next batch reloads them (r = 20 fits 160 KB this way)
+  double* scr = sU;
   if (__hip_atomic_load(C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   for (int o = tid; o < R * R; o += kCfNT) w_l[o] = C.w[o];
   const double is2 = 1.0 / P.signal_var;
@@ -495,7 +497,8 @@ size_t cf_lds_bytes(int r, int m) {
   const size_t base = 8 * (2 * (size_t)r * r + 4 * (size_t)m * r + m) + 4 * (2 * (size_t)m + 2);
   const size_t nn = 2 * (size_t)r;
   const size_t stf = 8 * (3 * (size_t)r * r + 7 * nn * nn + 7 * (size_t)r * r + nn * r + r) + 16;
-  return al16(base) + stf;
+  const size_t moves = 8 * 2 * (size_t)r * r + stf;      // w | wn | Stiefel scratch over the batch
+  return al16(base > moves ? base : moves);
 }
 
 
@@ -515,13 +518,9 @@ hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains
   switch (P.r) {
 #define CASE(RR)                                                                              \
   case RR: {                                                                                  \
-    static bool attr = false;                                                                 \
-    if (!attr) {                                                                              \
-      hipError_t e = hipFuncSetAttribute((const void*)cf_epoch_kernel<RR>,                     \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-      if (e != hipSuccess) return e;                                                          \
-      attr = true;                                                                            \
-    }                                                                                         \
+    static std::atomic<uint64_t> attr{0};                                                         \
+    hipError_t e = set_max_lds_once((const void*)cf_epoch_kernel<RR>, 160 * 1024, attr);          \
+    if (e != hipSuccess) return e;                                                                \
     hipLaunchKernelGGL(cf_epoch_kernel<RR>, dim3(nchains), dim3(kCfNT), lds, st, P, chains,   \
                        step0, nb);                                                            \
   } break;

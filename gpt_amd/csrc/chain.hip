@@ -165,7 +165,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
   const int start = b * m;
   const int Bt = min(m, P.N - start);
-  const int32_t* ord = Cp->order + (size_t)e * P.N + start;
+  const int32_t* ord = Cp->order + (size_t)(e & 1) * P.N + start;
   const long long koff = (long long)n * k, rstride = (long long)n * D;
   const double* phi_k = uni_ptr(Cp->phi) + koff;
   // Stage rows g0n .. g0n+G-1 of this wave's dimension into pw (lane-linear LDS image: double j
@@ -704,14 +704,10 @@ hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchain
   dim3 grid(nchains), block(64 * P.D);
 #define CASE_W(RR, JJ, WW)                                                                    \
   if (P.r == RR && J == JJ && (P.D <= 4) == (WW == 4)) {                                      \
-    static bool attr = false;                                                                 \
-    if (!attr) {                                                                              \
-      hipError_t e = hipFuncSetAttribute((const void*)chain_kernel<RR, JJ, kChainG, WW>,      \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize,          \
-                                         (int)(160 * 1024 - chain_static_lds(JJ, WW)));       \
-      if (e != hipSuccess) return e;                                                          \
-      attr = true;                                                                            \
-    }                                                                                         \
+    static std::atomic<uint64_t> attr{0};                                                     \
+    hipError_t e = set_max_lds_once((const void*)chain_kernel<RR, JJ, kChainG, WW>,           \
+                                    (int)(160 * 1024 - chain_static_lds(JJ, WW)), attr);      \
+    if (e != hipSuccess) return e;                                                            \
     hipLaunchKernelGGL((chain_kernel<RR, JJ, kChainG, WW>), grid, block, lds, st, P, chains, tbase, \
                        t_local);                                                              \
     return hipGetLastError();                                                                 \

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include <string>
 #include <vector>
 #include "gpt_common.h"
@@ -25,7 +26,8 @@ constexpr int kEngineChain = 1;    // chain.hip: one workgroup per chain, one ba
 struct ChainDesc {
   const double* phi;     // n*D*N   training features, Julia layout
   const double* y;       // N       training targets
-  const int32_t* order;  // E*N     cumulative epoch orders (0-based rows), see host
+  int32_t* order;        // 2*N     ring of cumulative epoch orders (0-based rows): order_e at
+                         //         (e&1)*N, built on the device (order.hip)
   double* w;             // 2*Q     ping-pong: w_t at (t&1)*Q
   double* U;             // n*r*D   current Stiefel factors (block k owns slice k)
   double* temp;          // 2*D*r*m ping-pong temp[k,l,i] of the NEXT batch
@@ -118,6 +120,20 @@ GPT_HD StepLayout step_layout(int n, int D, int r, int Q, int m) {
   return L;
 }
 
+// Raise a kernel's dynamic-LDS limit once per device.  Thread-safe: host threads (one per GPU, or
+// several sessions) may race to set the same attribute, which is idempotent; the latch only
+// skips the call once a device has it.
+inline hipError_t set_max_lds_once(const void* fn, int bytes, std::atomic<uint64_t>& latch) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const uint64_t bit = 1ull << (dev & 63);
+  if (latch.load(std::memory_order_acquire) & bit) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) latch.fetch_or(bit, std::memory_order_acq_rel);
+  return e;
+}
+
 // Host helpers (capi.hip / sgld.hip)
 void set_error(const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
@@ -135,6 +151,14 @@ hipError_t launch_step_cls(const StepParams& P, const ChainDesc* chains, int nch
 hipError_t launch_step_rms(const StepParams& P, const ChainDesc* chains, int nchains,
                            const long long* tbase, int t_local, hipStream_t st);
 hipError_t launch_advance(long long* tbase, long long by, hipStream_t st);
+// Epoch orders (order.hip): e_fixed >= 0 builds order_{e_fixed}; e_fixed < 0 builds order_{e+1}
+// for the epoch e of step tbase[0] + t_local.  ws: epoch_order_ws_ints(N, nchains) ints (0 when
+// the shuffle fits LDS).
+bool epoch_order_in_lds(int N);
+size_t epoch_order_ws_ints(int N, int nchains);
+hipError_t launch_epoch_order(const ChainDesc* chains, int nchains, int N, int nb,
+                              long long total_steps, const long long* tbase, int t_local,
+                              int e_fixed, int32_t* ws, hipStream_t st);
 bool rank_supported(int r);
 
 // Chain-resident engine (chain.hip): one workgroup per chain, many steps per launch.

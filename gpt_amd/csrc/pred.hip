@@ -467,13 +467,9 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
     if (!tile_vphase) {
       if (rlds > 64 * 1024) {
-        static bool attr = false;
-        if (!attr) {
-          e = hipFuncSetAttribute((const void*)pred_vphase_rows_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-          if (e != hipSuccess) break;
-          attr = true;
-        }
+        static std::atomic<uint64_t> attr{0};
+        e = set_max_lds_once((const void*)pred_vphase_rows_kernel, 160 * 1024, attr);
+        if (e != hipSuccess) break;
       }
       hipLaunchKernelGGL(pred_vphase_rows_kernel, vg, dim3(64), rlds, st, w + (size_t)s0 * Q, T,
                          offs, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest);
@@ -483,13 +479,9 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     switch (r) {
 #define CASE(RR)                                                                             \
   case RR: {                                                                                 \
-    static bool attr = false;                                                                \
-    if (!attr) {                                                                             \
-      e = hipFuncSetAttribute((const void*)pred_vphase_kernel<RR>,                           \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
-      if (e != hipSuccess) break;                                                            \
-      attr = true;                                                                           \
-    }                                                                                        \
+    static std::atomic<uint64_t> attr{0};                                                         \
+    e = set_max_lds_once((const void*)pred_vphase_kernel<RR>, 160 * 1024, attr);                  \
+    if (e != hipSuccess) break;                                                                   \
     hipLaunchKernelGGL(pred_vphase_kernel<RR>, vg, dim3(kNT), vlds, st, w + (size_t)s0 * Q, T, \
                        I0, D, Ntest, Q, fhat + (size_t)s0 * Ntest);                          \
     e = hipGetLastError();                                                                   \
@@ -512,13 +504,9 @@ static hipError_t launch_pred_direct(const double* w, const double* U, const int
   switch (r) {
 #define CASE(RR)                                                                             \
   case RR: {                                                                                 \
-    static bool attr = false;                                                                \
-    if (!attr) {                                                                             \
-      hipError_t e = hipFuncSetAttribute((const void*)pred_kernel<RR>,                        \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-      if (e != hipSuccess) return e;                                                         \
-      attr = true;                                                                           \
-    }                                                                                        \
+    static std::atomic<uint64_t> attr{0};                                                         \
+    hipError_t e = set_max_lds_once((const void*)pred_kernel<RR>, 160 * 1024, attr);              \
+    if (e != hipSuccess) return e;                                                                \
     hipLaunchKernelGGL(pred_kernel<RR>, grid, dim3(kNT), lds, st, w, U, I0, phitest, n, D,   \
                        Ntest, Q, fhat);                                                      \
   } break;
@@ -553,13 +541,9 @@ hipError_t launch_pred_x(const double* w, const double* U, const int32_t* I0, co
   switch (r) {
 #define CASE(RR)                                                                             \
   case RR: {                                                                                 \
-    static bool attr = false;                                                                \
-    if (!attr) {                                                                             \
-      hipError_t e = hipFuncSetAttribute((const void*)pred_x_kernel<RR>,                      \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-      if (e != hipSuccess) return e;                                                         \
-      attr = true;                                                                           \
-    }                                                                                        \
+    static std::atomic<uint64_t> attr{0};                                                         \
+    hipError_t e = set_max_lds_once((const void*)pred_x_kernel<RR>, 160 * 1024, attr);            \
+    if (e != hipSuccess) return e;                                                                \
     hipLaunchKernelGGL(pred_x_kernel<RR>, grid, dim3(kNT), lds, st, w, U, I0, X, ls, Z, bfe, c, \
                        n, D, Ntest, Q, fhat);                                                \
   } break;

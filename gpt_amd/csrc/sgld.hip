@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
   const int start = b * m;
   const int Bt = min(m, P.N - start);
-  const int32_t* ord = C.order + (size_t)e * P.N + start;
+  const int32_t* ord = C.order + (size_t)(e & 1) * P.N + start;
   const bool wblock = (k == D);
   STAMP(0);
 
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   const int s1 = b1 * m;
   const bool has_next = t1 < P.total_steps;
   const int B1 = has_next ? min(m, P.N - s1) : 0;
-  const int32_t* ord1 = C.order + (size_t)(has_next ? e1 : e) * P.N + (has_next ? s1 : start);
+  const int32_t* ord1 = C.order + (size_t)((has_next ? e1 : e) & 1) * P.N + (has_next ? s1 : start);
 
   // ---- P1: V, fhat, residual, A[:,k,:] (GPT_SGLD.jl:384-399)
   {
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
   const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
   const int start = b * m;
   const int Bt = min(m, P.N - start);
-  const int32_t* ord = C.order + (size_t)e * P.N + start;
+  const int32_t* ord = C.order + (size_t)(e & 1) * P.N + start;
   const double* Uk = C.U + (size_t)n * R * k;
   for (int o = tid; o < R * NP; o += kNT) {
     const int l = o / NP, j = o - l * NP;
@@ -624,9 +624,11 @@ hipError_t launch_advance(long long* tbase, long long by, hipStream_t st) {
 
 // Opt the kernels into >64 KiB of dynamic LDS once per process.
 hipError_t set_lds_limits() {
-  static bool done = false;
-  if (done) return hipSuccess;
-  hipError_t e = hipSuccess;
+  static std::atomic<uint64_t> done{0};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (done.load(std::memory_order_acquire) & (1ull << (dev & 63))) return hipSuccess;
 #define CASE(RR)                                                                              \
   e = hipFuncSetAttribute((const void*)sgld_step_kernel<RR>,                                   \
                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);            \
@@ -636,7 +638,7 @@ hipError_t set_lds_limits() {
   if (e != hipSuccess) return e;
   GPT_RANKS(CASE)
 #undef CASE
-  done = true;
+  done.fetch_or(1ull << (dev & 63), std::memory_order_acq_rel);
   return e;
 }
 

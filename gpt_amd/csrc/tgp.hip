@@ -534,13 +534,9 @@ static hipError_t launch_gmc_kick(const double* U, double* mom, const double* gU
   switch (r) {
 #define CASE(RR)                                                                              \
   case RR: {                                                                                  \
-    static bool attr = false;                                                                 \
-    if (!attr) {                                                                              \
-      hipError_t e = hipFuncSetAttribute((const void*)gmc_kick_kernel<RR>,                     \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-      if (e != hipSuccess) return e;                                                          \
-      attr = true;                                                                            \
-    }                                                                                         \
+    static std::atomic<uint64_t> attr{0};                                                         \
+    hipError_t e = set_max_lds_once((const void*)gmc_kick_kernel<RR>, 160 * 1024, attr);          \
+    if (e != hipSuccess) return e;                                                                \
     hipLaunchKernelGGL(gmc_kick_kernel<RR>, dim3(D), dim3(kNT), lds, st, U, mom, gU, c, n, init, \
                        seed, epoch);                                                          \
   } break;
@@ -557,13 +553,9 @@ static hipError_t launch_gmc_geod(double* U, double* mom, double t, int n, int D
   switch (r) {
 #define CASE(RR)                                                                              \
   case RR: {                                                                                  \
-    static bool attr = false;                                                                 \
-    if (!attr) {                                                                              \
-      hipError_t e = hipFuncSetAttribute((const void*)gmc_geod_kernel<RR>,                     \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-      if (e != hipSuccess) return e;                                                          \
-      attr = true;                                                                            \
-    }                                                                                         \
+    static std::atomic<uint64_t> attr{0};                                                         \
+    hipError_t e = set_max_lds_once((const void*)gmc_geod_kernel<RR>, 160 * 1024, attr);          \
+    if (e != hipSuccess) return e;                                                                \
     hipLaunchKernelGGL(gmc_geod_kernel<RR>, dim3(D), dim3(kNT), lds, st, U, mom, t, n, status); \
   } break;
     GPT_TGP_RANKS(CASE)

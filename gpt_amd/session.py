@@ -74,6 +74,11 @@ class SGLDSession:
     def run(self, nsteps):
         check(lib().gpt_sgld_session_run(self._h, int(nsteps)))
 
+    def prepare(self, nsteps):
+        """Capture the graphs the next ``run(nsteps)`` replays (nothing runs): a timed run then
+        launches graphs only."""
+        check(lib().gpt_sgld_session_prepare(self._h, int(nsteps)))
+
     def time_steps(self, nsteps):
         """Run nsteps un-captured steps with a hipEvent pair around every step-kernel launch;
         returns the mean step-kernel duration in microseconds."""

@@ -68,6 +68,10 @@ int gpt_feature_dev(const double* X_dev, int64_t N, int64_t D, const double* ls_
                     const double* b_dev, int64_t n, double* phi_dev, void* hip_stream);
 /* seeded Generation-C inputs of feature(X,n,ls,σ,seed,scale): Z=randn(n,D), b=2π·rand(n,D) */
 int gpt_feature_inputs(int64_t n, int64_t D, uint64_t seed, double* Z_out, double* b_out);
+/* seeded Generation-A inputs of feature(X,n,length_scale,seed)  GPT_SGLD_p.jl:40-54:
+ * Z = randn(n,D) (the Gen-C Z stream), b = randn(n,D) (its own stream); the caller applies
+ * Z/length_scale and scale sqrt(2/n) with sigma = 1 (gpt_feature with phi_scale = 1). */
+int gpt_feature_inputs_a(int64_t n, int64_t D, uint64_t seed, double* Z_out, double* b_out);
 
 /* samplenz(r,D,Q,seed)  GPT_SGLD.jl:181-190 / GPT_SGLD_p.jl:57-67  -> I (Q,D) Int32 1-based */
 int gpt_samplenz(int64_t r, int64_t D, int64_t Q, uint64_t seed, int32_t* I_out);
@@ -121,8 +125,12 @@ int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchains, const u
  * call before the first run. */
 int gpt_sgld_session_set_hyper(gpt_sgld_session* s, int32_t chain, double epsw, double epsU,
                                double signal_var, double sigma_w);
-/* Queue `nsteps` SGLD steps of every chain on the session stream (asynchronous). */
+/* Queue `nsteps` SGLD steps of every chain on the session stream (asynchronous).  Whole epochs
+ * replay one captured hipGraph; partial chunks replay a graph when one was prepared for them. */
 int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps);
+/* Capture (without running) the graphs a following gpt_sgld_session_run(s, nsteps) will replay,
+ * so that run launches no individual kernels and pays no capture inside a timed region. */
+int gpt_sgld_session_prepare(gpt_sgld_session* s, int64_t nsteps);
 /* Switch a grid-engine session (store_flags bit 2) to GPT_SGLDERM_RMSprop steps; call before
  * the first run. */
 int gpt_sgld_session_set_rmsprop(gpt_sgld_session* s, double epsilon, double alpha);
@@ -149,8 +157,9 @@ void gpt_sgld_session_destroy(gpt_sgld_session* s);
 /* out[4] = {engine (0 grid: D+1 workgroups per chain, 1 chain: one workgroup per chain),
  *           LDS bytes per workgroup, threads per workgroup, workgroups per step launch}.
  * store_flags of gpt_sgld_session_create: bit0 stores, bit1 diagnostics, bit2 force the grid
- * engine, bit3 force the chain engine (default: chain whenever the shape allows it; the
- * environment variable GPTSGLD_ENGINE=grid|chain overrides the default). */
+ * engine, bit3 force the chain engine (default: the grid engine while nchains*(D+1) workgroups
+ * fit the GPU's CUs — the shorter step — else the chain engine whenever the shape allows it;
+ * the environment variable GPTSGLD_ENGINE=grid|chain overrides the default). */
 int gpt_sgld_session_info(gpt_sgld_session* s, int64_t* out);
 
 /* ---- prediction ---------------------------------------------------------------------- */
@@ -243,6 +252,11 @@ int gpt_cf_fullw_gibbs(const double* Rating, int64_t N, int64_t ldr, int64_t n1,
                        double ytrainMean, double ytrainStd, int32_t avg, int32_t rotated_w,
                        double* w_store, double* U_store, double* V_store, double* testpred_store,
                        double* trainRMSE, double* testRMSE);
+
+/* randperm(N) + phi = phi[:,:,perm] of GPT_SGLD.jl:373-374 for `epochs` epochs of one chain,
+ * built on the device by the sessions' own kernel: out (N, epochs) column-major, 0-based rows
+ * of the composed order (order_e = order_{e-1}[perm_e]). */
+int gpt_epoch_orders(int64_t N, uint64_t seed, int64_t epochs, int32_t* out);
 
 const char* gpt_last_error(void);
 /* LDS bytes one step workgroup needs for this shape (must be <= 163840). */

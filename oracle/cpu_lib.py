@@ -1,0 +1,76 @@
+"""ctypes binding of oracle/_build/libgptcpu.so — the C++ fp64 restatement of GPT_SGLD.jl:345-448.
+
+TEST INFRASTRUCTURE and CPU BASELINE.  Only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import anything under ``oracle/``; the product path
+(``gpt_amd``) never does.  Built by ``make -C oracle`` (``__graft_entry__.build()``).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libgptcpu.so")
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("%s missing: run `make -C oracle`" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        P_D = C.POINTER(C.c_double)
+        L.gptcpu_regression.restype = C.c_longlong
+        L.gptcpu_regression.argtypes = [C.POINTER(C.c_int64), P_D, P_D, P_D, C.POINTER(C.c_int32),
+                                        C.c_int, C.POINTER(C.c_uint64), C.c_int, P_D, P_D, P_D, P_D,
+                                        C.POINTER(C.c_int32), P_D]
+        L.gptcpu_max_threads.restype = C.c_int
+        _LIB = L
+    return _LIB
+
+
+def _p(a, t=C.c_double):
+    return a.ctypes.data_as(C.POINTER(t)) if a is not None else None
+
+
+def GPTregression_chains(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, seeds,
+                         threads=1, sigma_w=1.0, store_every=1, max_steps=0, stores=False):
+    """Independent GPTregression chains (one per seed) on ``threads`` OpenMP threads.
+    Returns dict(w (Q, C), U (n, r, D, C), status (C,), steps, seconds[, w_store, U_store of
+    chain 0])."""
+    phi = np.asfortranarray(phi, dtype=np.float64)
+    n, D, N = phi.shape
+    y = np.ascontiguousarray(np.ravel(y), dtype=np.float64)
+    I = np.asfortranarray(I, dtype=np.int32)
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+    nch = len(seeds)
+    icfg = np.array([n, D, N, r, Q, m, burnin, maxepoch, store_every, max_steps], dtype=np.int64)
+    dcfg = np.array([epsw, epsU, signal_var, sigma_w], dtype=np.float64)
+    w = np.zeros((Q, nch), order="F")
+    U = np.zeros((n, r, D, nch), order="F")
+    nb = -(-N // m)
+    T = (maxepoch * nb) // store_every
+    ws = np.zeros((Q, T), order="F") if stores else None
+    Us = np.zeros((n, r, D, T), order="F") if stores else None
+    st = np.zeros(nch, dtype=np.int32)
+    sec = C.c_double(0.0)
+    steps = lib().gptcpu_regression(_p(icfg, C.c_int64), _p(dcfg), _p(phi), _p(y), _p(I, C.c_int32),
+                                    nch, _p(seeds, C.c_uint64), int(threads), _p(w), _p(U), _p(ws),
+                                    _p(Us), _p(st, C.c_int32), C.byref(sec))
+    if steps < 0:
+        raise ValueError("gptcpu_regression: unsupported configuration")
+    out = dict(w=w, U=U, status=st, steps=int(steps), seconds=sec.value)
+    if stores:
+        out.update(w_store=ws, U_store=Us)
+    return out
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"

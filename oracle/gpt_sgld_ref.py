@@ -76,6 +76,25 @@ def seeded_feature_inputs(n, D, seed):
     return Z, b
 
 
+def seeded_feature_inputs_a(n, D, seed):
+    """Generation-A seeded inputs (GPT_SGLD_p.jl:43-45): Z=randn(n,D) (the Gen-C Z stream),
+    b=randn(n,D) on the FEAT_B stream with c3 = 1."""
+    Z = px.normals(n * D, seed, 0, 9, 0).reshape((n, D), order="F")
+    b = px.normals(n * D, seed, 0, 10, 1).reshape((n, D), order="F")
+    return Z, b
+
+
+def feature_gen_a(X, n, length_scale, seed):
+    """GPT_SGLD_p.jl:40-54, line by line: Z = randn(n,D)/length_scale, b = randn(n,D),
+    phi[j,k,i] = cos(X[i,k]*Z[j,k] + b[j,k]), return sqrt(2/n)*phi (no sigma_RBF, no scale)."""
+    X = np.asarray(X, dtype=np.float64)
+    N, D = X.shape
+    Z, b = seeded_feature_inputs_a(n, D, seed)
+    Z = Z / float(length_scale)
+    phi = np.cos(X.T[None, :, :] * Z[:, :, None] + b[:, :, None])
+    return np.asfortranarray(math.sqrt(2.0 / n) * phi)
+
+
 # --------------------------------------------------------------------------- samplenz
 def samplenz_from_L(L, r, D):
     """GPT_SGLD.jl:181-190 body given the drawn lattice indices L:

@@ -57,6 +57,17 @@ def test_feature_inputs_host_matches_oracle():
     assert np.abs(Z - Zo).max() < 1e-15 and np.abs(b - bo).max() < 1e-15
 
 
+def test_feature_inputs_generation_a_host_matches_oracle():
+    """Gen A (GPT_SGLD_p.jl:43-45): b = randn(n,D), not 2π·rand."""
+    from gpt_amd import GPT_SGLD as G
+    Z, b = G.feature_inputs_a(30, 6, 17)
+    Zo, bo = R.seeded_feature_inputs_a(30, 6, 17)
+    assert np.abs(Z - Zo).max() < 1e-15 and np.abs(b - bo).max() < 1e-15
+    assert b.min() < 0.0                                   # normal, not uniform on [0, 2π)
+    Zc, _ = G.feature_inputs(30, 6, 17)
+    assert np.array_equal(Z, Zc)                           # the Z stream is shared with Gen C
+
+
 def test_bad_arguments_fail_without_device():
     from gpt_amd import GPT_SGLD as G
     from gpt_amd._lib import GPTError

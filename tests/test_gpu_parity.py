@@ -64,6 +64,30 @@ def test_feature_seeded_generation_c():
     assert rel(got, want) < 2e-15
 
 
+def test_feature_generation_a():
+    """feature(X,n,length_scale,seed) of GPT_SGLD_p.jl:40-54: b = randn, Z/ℓ, sqrt(2/n), no σ."""
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((70, 3))
+    got = G().feature(X, 24, 1.3, 11)
+    want = R.feature_gen_a(X, 24, 1.3, 11)
+    assert got.shape == (24, 3, 70)
+    assert np.abs(got - want).max() <= 1e-14 * np.abs(want).max()
+
+
+@pytest.mark.parametrize("N,seed,epochs", [(1, 3, 2), (2, 5, 3), (97, 1, 4), (5000, 17, 3),
+                                           (10000, 1001, 3), (13632, 2, 2), (20011, 7, 2)])
+def test_epoch_orders_match_oracle(N, seed, epochs):
+    """Device epoch orders (order.hip: parallel Fisher–Yates by reservations, LDS up to 13 632
+    rows, global workspace beyond) == the oracle's sequential randperm composed per epoch
+    (GPT_SGLD.jl:373-374), bit for bit."""
+    from oracle import philox as px
+    got = G().epoch_orders(N, seed, epochs)
+    order = np.arange(N)
+    for e in range(epochs):
+        order = order[px.randperm(N, seed, e)]
+        assert np.array_equal(got[:, e], order), "epoch %d" % e
+
+
 def test_feature_notensor_matches_oracle():
     rng = np.random.default_rng(3)
     N, D, n = 200, 4, 96
@@ -399,8 +423,10 @@ def test_multichain_session_equals_single_runs(engine):
     s = SGLDSession(phi_t, y_t, p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 2, seeds, store_every=2,
                     engine=engine)
     assert s.info()["engine"] == engine
-    s.run(3)          # partial chunk, then the rest through the captured graph
-    s.run(10 ** 9)
+    s.run(3)          # partial chunk (direct launches)
+    s.prepare(4)      # graphs for the next 4 steps: the epoch's last step + 3 of the next epoch
+    s.run(4)          # replays them (an epoch-order build inside the second graph)
+    s.run(10 ** 9)    # the rest
     s.sync()
     for c, sd in enumerate(seeds):
         ws, Us, st = s.fetch(c)
@@ -408,3 +434,18 @@ def test_multichain_session_equals_single_runs(engine):
                                     store_every=2)
         assert st == 0 and rel(ws, wo) < 1e-8 and rel(Us, Uo) < 1e-8
     s.close()
+
+
+@pytest.mark.parametrize("engine", ["grid", "chain"])
+def test_epoch_order_ring_over_many_epochs(engine):
+    """Seven epochs of a ragged N (nb = 4) with every epoch-end sample stored: the two-slot order
+    ring (order.hip) must hand each epoch its own composed permutation, through direct launches
+    and graph replays alike."""
+    n, D, N, r, Q, m = 24, 3, 29, 3, 10, 8
+    p = make_problem(n, D, N, r, Q, seed=31)
+    got_w, got_U = G().GPTregression(p["phi"], p["y"], 0.05, p["I"], r, Q, m, 1e-4, 1e-6, 1, 6, 9,
+                                     store_every=2, engine=engine)
+    wo, Uo, info = R.GPTregression(p["phi"], p["y"], 0.05, p["I"], r, Q, m, 1e-4, 1e-6, 1, 6, 9,
+                                   store_every=2)
+    assert info["status"] == 0
+    assert rel(got_w, wo) < 1e-8 and rel(got_U, Uo) < 1e-8

@@ -1,0 +1,144 @@
+"""Quality parity at the BASELINE configurations, on the GPU.
+
+* kin40k at the reference's own configuration (kin40kExperiment.jl:38-51,67-91: n = 150, r = 20,
+  Q = 200, m = 50, εw = 1e-4, εU = 1e-7, random length scales 1 + 0.2·randn per sweep): the
+  per-epoch test-RMSE curves of ten sweeps against the reference's recorded curve
+  (testRMSE_kin40k.h5 -> tests/golden/ref_curves.npz).  Julia's RNG stream is not reproducible,
+  so this is a band, not a per-value match: every surviving sweep within [0.85, 1.2]x the
+  reference curve over epochs 5-30 and the median within 10 % at epoch 30.  Sweeps that take the
+  geodesic NaN bail-out (GPT_SGLD.jl:422-424) are counted, as the reference's logs count
+  `RMSE=NaN` runs (DataRecords.txt:61,71,75,91); at least 6 of 10 must survive.
+* BASELINE config 1 (PowerPlantNoTensorExperiment.jl:5-42): full-theta SGLD on PowerPlant rows
+  1-5000, n = 2000 features, m = 50, εθ = 1.1e-4, 100 epochs — the whole trajectory against the
+  oracle (<= 1e-9 relative) and the script's "testRMSE with averaged pred" (epochs 60-100, :62-63)
+  against the exact-GP ceiling 4.0056 (DataRecords.txt:19): within [3.95, 4.35].
+* BASELINE config 5 at r = 20 (100k_movielensExperiment.jl): GPT_fullw_sideinfo for one epoch of
+  fold 1 (80 000 ratings; the live configuration of :723-730 at r = 20) and an SGLD + Stiefel run,
+  and GPT_fullw_gibbs (r² = 400 Kronecker design), against the oracle.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import gpt_sgld_ref as R
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rel(a, b):
+    a = np.asarray(a); b = np.asarray(b)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+
+
+def test_kin40k_reference_configuration_tracks_reference_curve():
+    import torch
+    from bench import kin40k
+    from gpt_amd import GPT_SGLD as G
+    from gpt_amd.session import SGLDSession, feature_device, pred_device
+
+    dev = torch.device("cuda", 0)
+    n, D, r, Q, m, epochs, sweeps = 150, 8, 20, 200, 50, 30, 10
+    Xtr, ytr, Xte, yte, ysd = kin40k(D)
+    N, Nte = Xtr.shape[0], Xte.shape[0]
+    nb = -(-N // m)
+    I = G.samplenz(r, D, Q, 17)                                 # kin40kExperiment.jl:44
+    scale = math.sqrt(n / Q ** (1.0 / D))                       # :45
+    Z, b = G.feature_inputs(n, D, 17)
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    Xtr_d, Xte_d, Z_d, b_d = tt(Xtr.T), tt(Xte.T), tt(Z.T), tt(b.T)
+    phis, phites = [], []
+    for j in range(1, sweeps + 1):                              # :67-72
+        g = np.random.default_rng(j)
+        ls = np.ones(D) + 0.2 * g.standard_normal(D)
+        srbf = 1 + 0.2 * g.standard_normal()
+        phis.append(feature_device(Xtr_d, tt(ls), srbf, scale, Z_d, b_d))
+        phites.append(feature_device(Xte_d, tt(ls), srbf, scale, Z_d, b_d))
+    sess = SGLDSession(phis, tt(ytr), I, r, Q, m, 1e-4, 1e-7, 0.0476, 0, epochs,
+                       list(range(1, sweeps + 1)), store_every=nb, store=True)
+    sess.run(epochs * nb)
+    sess.sync()
+    I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
+    yte_d = tt(yte)
+    fh = torch.empty((epochs, Nte), dtype=torch.float64, device=dev)
+    ref = np.load(os.path.join(ROOT, "tests", "golden", "ref_curves.npz"))["testRMSE_kin40k"]
+    curves, alive = [], 0
+    for c in range(sweeps):
+        if sess.fetch(c)[2] != 0:                               # NaN bail-out: zero stores
+            continue
+        alive += 1
+        _, _, ws, Us, ns = sess.device_state(c)
+        assert ns == epochs
+        pred_device(ws, Us, I0, phites[c], n, D, Nte, r, Q, epochs, fh)
+        err = fh - yte_d[None, :]
+        curves.append((ysd * torch.sqrt((err * err).mean(dim=1))).cpu().numpy())   # :83
+    sess.close()
+    assert alive >= 6, "only %d of %d sweeps survived" % (alive, sweeps)
+    curves = np.array(curves)
+    ratio = curves[:, 4:30] / ref[4:30][None, :]
+    assert ratio.min() >= 0.85 and ratio.max() <= 1.2, (ratio.min(), ratio.max())
+    assert abs(np.median(curves[:, 29]) / ref[29] - 1.0) <= 0.10
+    assert np.all(curves[:, 29] < curves[:, 0])                 # every sweep learns
+
+
+def test_gpnt_sgld_config1_powerplant_full_run():
+    from bench import powerplant
+    from gpt_amd import GPT_SGLD as G
+    Xtr, ytr, Xte, yte, ysd = powerplant(4)                      # :5-26 (whitened, 5000 rows)
+    n, m, eps, epochs = 2000, 50, 0.00011, 100
+    phi = G.featureNotensor(Xtr, n, 1.4332, 1.0, 17)             # :32
+    phite = G.featureNotensor(Xte, n, 1.4332, 1.0, 17)           # :33
+    Z, b = R.seeded_feature_inputs(n, 4, 17)
+    phi_o = R.featureNotensor(Xtr, 1.4332, 1.0, Z, b[:, 0])
+    assert rel(phi, phi_o) < 1e-14                  # same argument bits; cos differs by ulps
+    got = G.GPNT_SGLD(phi, ytr, 0.2299 ** 2, 1.0, m, eps, 0, 0, epochs, 1)    # :42
+    want = R.GPNT_SGLD(phi, ytr, 0.2299 ** 2, 1.0, m, eps, 0, 0, epochs, 1)
+    assert got.shape == want.shape == (n, epochs * 100)
+    assert rel(got, want) < 1e-9
+    nb = 100
+    fh = np.stack([phite.T @ got[:, nb * e - 1] for e in range(1, epochs + 1)], axis=1)   # :53-56
+    mean_fhat = fh[:, 59:100].mean(axis=1)                                               # :62
+    rmse = ysd * math.sqrt(np.mean((mean_fhat - yte) ** 2))                              # :63
+    assert 3.95 <= rmse <= 4.35, rmse
+
+
+def _ml(ntr, nte, fold=1):
+    from gpt_amd import movielens
+    d = np.load(os.path.join(ROOT, "tests", "golden", "ml100k.npz"))
+    tr, te, ud, md, mu, sd = movielens.fold(d, fold)
+    return tr[:ntr], te[:nte], ud, md, mu, sd
+
+
+@pytest.mark.parametrize("ntr,nte,m,ep,lang,stf,epsU", [
+    (80000, 20000, 100, 1, False, False, 1e-6),          # live configuration of :723-730, r = 20
+    (6000, 1500, 64, 2, True, True, 1e-4),               # SGLD + Stiefel
+])
+def test_movielens_sideinfo_r20_matches_oracle(ntr, nte, m, ep, lang, stf, epsU):
+    from gpt_amd import movielens
+    from oracle import movielens_ref as M
+    tr, te, ud, md, mu, sd = _ml(ntr, nte)
+    w0 = np.random.default_rng(17).standard_normal((20, 20))
+    args = (tr, ud, md, te, 0.8, 0.1, 1.0, w0, m, 1e-4, epsU, 0.5, 0.25, 0.5, 0, ep, 17, mu, sd)
+    got = movielens.GPT_fullw_sideinfo(*args, langevin=lang, stiefel=stf)
+    want = M.GPT_fullw_sideinfo(*args, langevin=lang, stiefel=stf)
+    for g, w_ in zip(got[:3], want[:3]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    assert np.abs(got[3] - want[3]).max() < 1e-8
+    assert np.all(np.abs(got[5] - want[5]) <= 1e-9 * want[5])
+    assert 0.8 < got[5][0] < 1.4                                 # rating-scale test RMSE
+
+
+def test_movielens_gibbs_r20_matches_oracle():
+    from gpt_amd import movielens
+    from oracle import movielens_ref as M
+    tr, te, ud, md, mu, sd = _ml(6000, 1500)
+    w0 = np.random.default_rng(9).standard_normal((20, 20))
+    args = (tr, ud, md, te, 0.8, 0.5, 1.0, w0, 0, 2, 1, 17, mu, sd)
+    got = movielens.GPT_fullw_gibbs(*args)
+    want = M.GPT_fullw_gibbs(*args)
+    for g, w_ in zip(got[:3], want[:3]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    assert np.abs(got[3] - want[3]).max() < 1e-8
+    assert np.all(np.abs(got[5] - want[5]) <= 1e-9 * want[5])
