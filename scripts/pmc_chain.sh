@@ -3,9 +3,9 @@
 # combined with sys/runtime traces), summarised by scripts/pmc_chain_summary.py.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc_chain
+OUT=gpurun_out/pmc_chain_${TAG:-x}
 mkdir -p $OUT
-ARGS="--engine chain --steps 200 --warmup 50 --no-cpu-baseline ${BENCH_ARGS:-}"
+ARGS="--engine chain --steps 200 --warmup 50 --epochs 1 --no-single-chain --no-cpu-baseline ${BENCH_ARGS:-}"
 i=0
 for PMC in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
