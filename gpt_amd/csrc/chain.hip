@@ -88,40 +88,19 @@ struct ChainLds {
       P.stamps[(size_t)blockIdx.x * kStamps + (slot)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 
+// Loop sub-phase stamps (diagnostic runs only): waves 0 and 4 (one SIMD) at one row group, in the
+// stamp row gridDim.x + blockIdx.x (the library sizes the stamp buffer for D+1 rows per chain).
+#define LSTAMP(slot)                                                                        \
+  do {                                                                                      \
+    if (P.stamps && g0 == 20 && lane == 0 && (k == 0 || k == 4))                            \
+      P.stamps[(size_t)(gridDim.x + blockIdx.x) * kStamps + (k ? 8 : 0) + (slot)] =         \
+          (long long)__builtin_amdgcn_s_memtime();                                         \
+  } while (0)
+
 // Workgroup barrier that orders LDS only: an LDS-DMA prefetch stays in flight across it
 // (__syncthreads() would also drain vmcnt).
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// Wave-wide sums of NV per-lane values written to dst[0..NV) (and, with dst2, values NV..2NV-1
-// to dst2[0..NV)); the caller orders the LDS writes with wave_sync().
-template <int NV>
-__device__ __forceinline__ void wave_sum_to_lds(double (&v)[NV], double* dst) {
-  constexpr int NB = NV <= 8 ? 8 : (NV <= 16 ? 16 : (NV <= 32 ? 32 : 64));
-  const int lane = threadIdx.x & 63;
-  double b[NB];
-#pragma unroll
-  for (int x = 0; x < NB; ++x) b[x] = x < NV ? v[x] : 0.0;
-  Butterfly<NB>::run(b, lane);
-  constexpr int SH = 6 - Butterfly<NB>::P;
-  const int vi = lane >> SH;
-  if ((lane & ((1 << SH) - 1)) == 0 && vi < NV) dst[vi] = b[0];
-}
-template <int NV>
-__device__ __forceinline__ void wave_sum_to_lds(double (&v)[2 * NV], double* dst, double* dst2) {
-  constexpr int NB = 2 * NV <= 8 ? 8 : (2 * NV <= 16 ? 16 : (2 * NV <= 32 ? 32 : 64));
-  const int lane = threadIdx.x & 63;
-  double b[NB];
-#pragma unroll
-  for (int x = 0; x < NB; ++x) b[x] = x < 2 * NV ? v[x] : 0.0;
-  Butterfly<NB>::run(b, lane);
-  constexpr int SH = 6 - Butterfly<NB>::P;
-  const int vi = lane >> SH;
-  if ((lane & ((1 << SH) - 1)) == 0 && vi < 2 * NV) {
-    if (vi < NV) dst[vi] = b[0];
-    else dst2[vi - NV] = b[0];
-  }
 }
 
 // WV: waves per workgroup the build is bounded for — kChainDMax, or 4 for D <= 4, where one wave
@@ -297,8 +276,10 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     // loop instead of being hoisted into registers that stay live across it
     int ln = lane;
     asm volatile("" : "+v"(ln));
+    LSTAMP(0);
     // (a) this wave's staged rows -> registers, then stage the next group behind them
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LSTAMP(1);
     double* pw = pw0 + (CHAIN_DBUF ? slot * (G * 64 * J) : 0);
 #if CHAIN_DBUF
     if (g0 + G < Bt) stage(g0 + G, ln, pw0 + (slot ^ 1) * (G * 64 * J));
@@ -310,6 +291,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       for (int jj = 0; jj < J; ++jj)
         p[gg][jj] = pw[gg * 64 * J + ln + 64 * jj];   // j >= n: finite in-row values, u = 0 there
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    LSTAMP(2);
 #if CHAIN_STAGE_AT == 0 && !CHAIN_DBUF
     if (g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
@@ -348,7 +330,9 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 #if CHAIN_STAGE_AT == 3 && !CHAIN_DBUF
     if (!CHAIN_EXP_NOSTAGE && g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
+    LSTAMP(3);
     lds_barrier();
+    LSTAMP(4);
 #if CHAIN_STAGE_AT == 1 && !CHAIN_DBUF
     if (g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
@@ -378,7 +362,9 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 #if CHAIN_STAGE_AT == 4 && !CHAIN_DBUF
     if (g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
+    LSTAMP(5);
     lds_barrier();
+    LSTAMP(6);
 #if CHAIN_STAGE_AT == 2 && !CHAIN_DBUF
     if (!CHAIN_EXP_NOSTAGE && g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
@@ -426,6 +412,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       for (int g2 = 1; g2 < G; ++g2) if (gg == g2) rr = res[g2];
       gw[x] = fma(vsave[x], rr, gw[x]);
     }
+    LSTAMP(7);
   }
   CSTAMP(2);
 

@@ -501,6 +501,36 @@ __device__ __forceinline__ void wave_solve_body(double* M, double* X, long long*
   wave_sync();
 }
 
+// Wave-wide sums of NV per-lane values written to dst[0..NV) (and, with dst2, values NV..2NV-1
+// to dst2[0..NV)); the caller orders the LDS writes with wave_sync().
+template <int NV>
+__device__ __forceinline__ void wave_sum_to_lds(double (&v)[NV], double* dst) {
+  constexpr int NB = NV <= 8 ? 8 : (NV <= 16 ? 16 : (NV <= 32 ? 32 : 64));
+  const int lane = threadIdx.x & 63;
+  double b[NB];
+#pragma unroll
+  for (int x = 0; x < NB; ++x) b[x] = x < NV ? v[x] : 0.0;
+  Butterfly<NB>::run(b, lane);
+  constexpr int SH = 6 - Butterfly<NB>::P;
+  const int vi = lane >> SH;
+  if ((lane & ((1 << SH) - 1)) == 0 && vi < NV) dst[vi] = b[0];
+}
+template <int NV>
+__device__ __forceinline__ void wave_sum_to_lds(double (&v)[2 * NV], double* dst, double* dst2) {
+  constexpr int NB = 2 * NV <= 8 ? 8 : (2 * NV <= 16 ? 16 : (2 * NV <= 32 ? 32 : 64));
+  const int lane = threadIdx.x & 63;
+  double b[NB];
+#pragma unroll
+  for (int x = 0; x < NB; ++x) b[x] = x < 2 * NV ? v[x] : 0.0;
+  Butterfly<NB>::run(b, lane);
+  constexpr int SH = 6 - Butterfly<NB>::P;
+  const int vi = lane >> SH;
+  if ((lane & ((1 << SH) - 1)) == 0 && vi < 2 * NV) {
+    if (vi < NV) dst[vi] = b[0];
+    else dst2[vi - NV] = b[0];
+  }
+}
+
 __device__ __forceinline__ double readlane_d(double v, int lane) {
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);

@@ -168,6 +168,7 @@ size_t chain_lds_bytes(int n, int D, int r, int Q, int m);
 hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchains,
                         const long long* tbase, int t_local, hipStream_t st);
 
+
 hipError_t launch_pred_x(const double* w, const double* U, const int32_t* I0, const double* X,
                          const double* ls, const double* Z, const double* bfe, double c, int n,
                          int D, long long Ntest, int r, int Q, int S, double* fhat, hipStream_t st);

@@ -55,6 +55,7 @@ def main():
         # workgroup c writes slot c of it
         out = np.zeros((args.steps, (D + 1) * args.chains, 16), dtype=np.int64)
         check(lib().gpt_sgld_session_stamps(s._h, args.steps, out.ctypes.data_as(C.POINTER(C.c_int64))))
+        lp = out[:, args.chains:2 * args.chains, :]
         out = out[:, :args.chains, :]
         tot = np.median((out[..., 7] - out[..., 0]).ravel())
         print("chain engine: median cycles per phase (wave 0), batch of %d rows" % m)
@@ -68,6 +69,15 @@ def main():
         arr = out[..., 8:16] - out[..., 0:1]
         print("  per-wave arrival at the end-of-step barrier (cycles from start):",
               " ".join("%d" % v for v in np.median(arr.reshape(-1, 8), axis=0)))
+        if (lp[..., 7] > 0).all():
+            names = ["vmcnt wait (row DMA)", "(a) rows LDS->regs", "(b) temp + reductions",
+                     "barrier 1", "(c) V task", "barrier 2", "(e) residual, A, gradU"]
+            for wv, base in (("wave 0", 0), ("wave 4", 8)):
+                d = np.median(lp[..., base + 1:base + 8] - lp[..., base:base + 7], axis=(0, 1))
+                print("  loop group 10, %s: " % wv + ", ".join("%s %d" % (nm, v) for nm, v in zip(names, d))
+                      + "  (total %d)" % np.median(lp[..., base + 7] - lp[..., base]))
+            print("  wave 4 starts the group %d cycles after wave 0"
+                  % np.median(lp[..., 8] - lp[..., 0]))
         print("event-timed step kernel: %.2f us" % s.time_steps(20))
         return
     nb = (D + 1) * args.chains

@@ -156,6 +156,12 @@ CASES = {
     "ref_kin40k_rank20": (150, 8, 100, 20, 200, 50, 0, 1, 1, True, True),
     "batch256": (96, 4, 600, 5, 80, 256, 0, 1, 1, True, True),
     "powerplant_shape": (500, 4, 600, 5, 200, 256, 0, 2, 1, True, True),   # D <= 4 build, J = 8, 2 V tasks/wave
+    # odd shapes of the chain engine at D >= 5: half-filled 64-row blocks, ragged batches,
+    # the n = 512 / Q = 256 maxima (a 64-member run), thinning after burn-in
+    "c2_d5_half128": (200, 5, 90, 3, 70, 20, 0, 2, 1, True, True),      # J2 = 2, ragged last batch
+    "c2_n258_thin": (258, 6, 60, 4, 130, 15, 1, 2, 3, True, True),      # 2 rows in the second half
+    "c2_n512_q256": (512, 8, 70, 5, 256, 33, 0, 1, 1, True, True),      # full halves, 8 V tasks, odd m
+    "c2_r2_d7": (300, 7, 64, 2, 100, 16, 0, 2, 2, True, True),
 }
 
 
@@ -164,8 +170,12 @@ def _chain_ok(n, D, r, lang, stf):
     return lang and stf and D <= 8 and r <= 5 and n <= 512
 
 
+def _shape(name):
+    return [CASES[name][i] for i in (0, 1, 3, 9, 10)]
+
+
 ENGINE_CASES = [(name, eng) for name in CASES for eng in ("grid", "chain")
-                if eng == "grid" or _chain_ok(*[CASES[name][i] for i in (0, 1, 3, 9, 10)])]
+                if eng == "grid" or _chain_ok(*_shape(name))]
 
 
 @pytest.mark.parametrize("name,engine", ENGINE_CASES)
@@ -195,8 +205,8 @@ def test_sampler_trajectory_matches_oracle(name, engine):
 
 @pytest.mark.parametrize("name", [c for c, e in ENGINE_CASES if e == "chain"])
 def test_chain_trajectory_without_diagnostics(name):
-    """Without per-step gradient norms the chain engine folds the U noise into the gradient
-    accumulator inside the batch loop (chain.hip, noise_block): same samples as the oracle."""
+    """The chain engine with no per-step gradient-norm buffer (the diag writes compiled in but
+    skipped, the production configuration): same samples as the oracle."""
     n, D, N, r, Q, m, burnin, maxepoch, se, lang, stf = CASES[name]
     p = make_problem(n, D, N, r, Q, seed=11)
     epsw, epsU, sv, seed = 1e-4, 1e-6, 0.05, 23
