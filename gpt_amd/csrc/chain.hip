@@ -50,7 +50,7 @@ constexpr int kChainMMax = 256;   // largest minibatch the engine takes
 
 // Per-wave scratch after the batch: S0 = max(expm<2r> scratch, noise slots) | E[:,1:r] | grams.
 GPT_HD constexpr int chain_scratch_dbl(int r) {
-  const int s0a = 7 * 4 * r * r, s0b = 64 * (r + (r & 1));
+  const int s0a = 7 * 4 * r * r, s0b = 64 * 8;     // expm scratch | noise slots (8 row blocks)
   return (s0a > s0b ? s0a : s0b) + 2 * r * r + 3 * r * r + r;
 }
 GPT_HD constexpr int al16c(int x) { return (x + 15) & ~15; }
@@ -459,27 +459,37 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   const double cU = cN / C.signal_var;
   const double sq = sqrt(C.epsU);
   double gu2 = 0.0;
-  constexpr int RE = R + (R & 1);
-#pragma unroll
-  for (int jj = 0; jj < J; ++jj) {
-    const int j = lane + 64 * jj;
-    // noise pairs through this lane's LDS slots: one non-unrolled Philox/Box–Muller body
-    // (register-light) instead of J·R/2 interleaved copies next to the live U / gradU tiles
-    {
-      const int jc = j < n ? j : n - 1;
+  // U noise on the quad contract (gpt_common.h): lane λ's rows λ + 64·jj are exactly the rows of
+  // its quads, so every Box–Muller output is used.  One non-unrolled column loop (register-light
+  // Philox/Box–Muller body, values through this lane's LDS slots); the column's drive is applied
+  // under a uniform branch so the accumulator registers keep static indices.
+  {
+    constexpr int NQJ = (J + 3) / 4;
+    constexpr int NZ = J >= 4 ? 4 : 2;
+    const int NQ = unoise_nq(n);
 #pragma unroll 1
-      for (int l = 0; l < R; l += 2) {
-        double z0, z1;
-        normal_pair(C.seed, (uint32_t)((l + RE * jc) >> 1), (uint32_t)t, kUNoise, (uint32_t)k, z0, z1);
-        xi_l[lane * RE + l] = z0;
-        xi_l[lane * RE + l + 1] = z1;
-      }
-    }
-#pragma unroll
     for (int l = 0; l < R; ++l) {
-      const double Gv = j < n ? acc[jj][l] * cU : 0.0;
-      gu2 = fma(Gv, Gv, gu2);
-      acc[jj][l] = j < n ? sq * Gv / 2 + xi_l[lane * RE + l] : 0.0;    // :420 drive
+#pragma unroll
+      for (int q = 0; q < NQJ; ++q) {
+        double z[4];
+        normal_quad<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
+                        (uint32_t)k, z);
+#pragma unroll
+        for (int i = 0; i < NZ; ++i)
+          if (4 * q + i < J) xi_l[(4 * q + i) * 64 + lane] = z[i];
+      }
+#pragma unroll
+      for (int L = 0; L < R; ++L) {
+        if (l == L) {
+#pragma unroll
+          for (int jj = 0; jj < J; ++jj) {
+            const int j = lane + 64 * jj;
+            const double Gv = j < n ? acc[jj][L] * cU : 0.0;
+            gu2 = fma(Gv, Gv, gu2);
+            acc[jj][L] = j < n ? sq * Gv / 2 + xi_l[jj * 64 + lane] : 0.0;    // :420 drive
+          }
+        }
+      }
     }
   }
   if (C.diag) {
@@ -489,7 +499,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   CSTAMP(4);
   {
     constexpr int NN = 2 * R;
-    constexpr int S0 = (7 * NN * NN > 64 * RE) ? 7 * NN * NN : 64 * RE;
+    constexpr int S0 = (7 * NN * NN > 64 * 8) ? 7 * NN * NN : 64 * 8;
     double* X0 = X;                          // expm scratch (7·NN²), reused for expm(−tA)
     double* Ec = X + S0;                     // E[:, 0:r]  (NN × R)
     double* Mg = Ec + NN * R;                // UᵀW, then Ag | Sg | nrm

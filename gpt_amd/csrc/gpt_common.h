@@ -79,6 +79,39 @@ __device__ __forceinline__ void normal_pair(uint64_t seed, uint32_t c0, uint32_t
   z1 = rad * sn;
 }
 
+// U-noise contract (oracle/philox.py, U_NOISE): rows of the n×r noise matrix of one dimension
+// come in blocks of 64 (row j = λ + 64·b); the Philox block at
+//   c0 = (l·NQ + q)·64 + λ,   NQ = ⌈⌈n/64⌉/4⌉,
+// gives column l of rows λ + 64·(4q + i), i = 0..3, as two Box–Muller pairs of 32-bit uniforms:
+//   (z0, z1) = √(−2 ln u(x0))·(cos 2πu(x1), sin 2πu(x1)),  (z2, z3) likewise from (x2, x3),
+//   u(x) = (x + ½)·2⁻³².  Rows ≥ n are dropped.
+// One Philox call feeds four normals, and a wave whose lane λ owns rows λ + 64·b (the chain
+// engine) draws exactly its own elements.
+GPT_HD int unoise_nq(int n) { return ((n + 63) / 64 + 3) / 4; }
+GPT_HD double u32u(uint32_t x) { return ((double)x + 0.5) * (1.0 / 4294967296.0); }
+
+// NZ = 4: both pairs; NZ = 2: the first pair only (blocks 4q+2, 4q+3 past the last row block).
+template <int NZ>
+__device__ __forceinline__ void normal_quad(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2,
+                                            uint32_t c3, double* z) {
+  const U4 x = philox4x32(c0, c1, c2, c3, seed);
+  const auto c = fm_coef();
+  {
+    const double rad = sqrt(-2.0 * fm_log_c(u32u(x.x), c));
+    double sn, cs;
+    fm_sincos_2pi_c(u32u(x.y), sn, cs, c);
+    z[0] = rad * cs;
+    z[1] = rad * sn;
+  }
+  if constexpr (NZ == 4) {
+    const double rad = sqrt(-2.0 * fm_log_c(u32u(x.z), c));
+    double sn, cs;
+    fm_sincos_2pi_c(u32u(x.w), sn, cs, c);
+    z[2] = rad * cs;
+    z[3] = rad * sn;
+  }
+}
+
 // Global-address-space view of a pointer (global_load/global_store instead of flat_*, which
 // would also count against lgkmcnt and serialise behind LDS traffic).
 template <class T>

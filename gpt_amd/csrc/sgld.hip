@@ -230,10 +230,27 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     coef_l[l * MP + i] *= res_l[i];
   }
   const double* Ug = C.U + (size_t)n * R * k;
+  // W_l starts as the Langevin noise ξ of the drive (quad contract, gpt_common.h): the quads are
+  // spread over the threads here, so P2's thread-per-row drive reads its ξ[j, :] from LDS
+  const bool noise0 = (P.langevin || P.ncls) && !P.rms;
   for (int o = tid; o < R * NP; o += kNT) {
     const int l = o / NP, j = o - l * NP;
     U_l[l * NS + j] = j < n ? gptr(Ug)[j + (size_t)n * l] : 0.0;
-    W_l[l * NS + j] = 0.0;
+    if (j >= n || !noise0) W_l[l * NS + j] = 0.0;
+  }
+  if (noise0) {
+    const uint32_t c3 = P.ncls ? (uint32_t)(k + D * 2 * (blockIdx.y % P.ncls)) : (uint32_t)k;
+    const int NQ = unoise_nq(n);
+    for (int qd = tid; qd < R * NQ * 64; qd += kNT) {
+      const int l = qd / (NQ * 64), q = (qd >> 6) - l * NQ, lam = qd & 63;
+      double z[4];
+      normal_quad<4>(C.seed, (uint32_t)qd, (uint32_t)t, kUNoise, c3, z);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = lam + 64 * (4 * q + i);
+        if (j < n) W_l[l * NS + j] = z[i];
+      }
+    }
   }
   __syncthreads();
   STAMP(3);
@@ -251,7 +268,6 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     double acc[R];
 #pragma unroll
     for (int l = 0; l < R; ++l) acc[l] = 0.0;
-    double xi[R];
     for (int i0 = 0; i0 < Bt; i0 += 32) {
       const int vrow = batch_rows_lane(ord, 0, i0, Bt);      // lane u: row of column i0+u
       double p[32];
@@ -259,20 +275,6 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       for (int u = 0; u < 32; ++u) {
         const int row = __builtin_amdgcn_readlane(vrow, u);  // columns past Bt: clamped row
         p[u] = (gptr(C.phi) + koff + (long long)row * rstride)[jc];
-      }
-      if (i0 == 0) {   // Langevin noise (ALU) while the loads are in flight
-        // U-noise contract: ξ[j,l] = element l + RE·j of stream (t, U_NOISE, k), RE = R rounded
-        // up to even, so one Box–Muller pair serves (l, l+1) of the same row j.
-        constexpr int RE = R + (R & 1);
-        const uint32_t c3 = P.ncls ? (uint32_t)(k + D * 2 * (blockIdx.y % P.ncls)) : (uint32_t)k;
-#pragma unroll
-        for (int l = 0; l < R; l += 2) {
-          double z0 = 0.0, z1 = 0.0;
-          if (P.langevin || P.ncls)
-            normal_pair(C.seed, (uint32_t)((l + RE * jc) >> 1), (uint32_t)t, kUNoise, c3, z0, z1);
-          xi[l] = z0;
-          if (l + 1 < R) xi[l + 1] = z1;
-        }
       }
 #pragma unroll
       for (int u = 0; u < 32; ++u)
@@ -298,10 +300,10 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
         gn2 = fma(G, G, gn2);
         if (P.ncls) gptr_w(C.gU)[(size_t)n * R * k + (size_t)n * l + j] = G;   // second move
         if (P.stiefel || P.ncls) {
-          W_l[l * NS + j] = sq * G / 2 + xi[l];                  // :420 drive
+          W_l[l * NS + j] = sq * G / 2 + W_l[l * NS + j];         // :420 drive (W_l held ξ)
         } else {                                                  // :426 / :437
           const double u = U_l[l * NS + j];
-          U_l[l * NS + j] = u + (C.epsU * (G - n * u) / 2 + sq * xi[l]);
+          U_l[l * NS + j] = u + (C.epsU * (G - n * u) / 2 + sq * W_l[l * NS + j]);
         }
       }
     }
@@ -314,14 +316,15 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   if (P.rms) {
     __syncthreads();
     sk = sqrt(blk_sum(esum, red) / ((double)n * R));
-    constexpr int RE = R + (R & 1);
-    for (int j = tid; j < n; j += kNT) {       // drive √εU_k·gradU/2 + ξ (:1231)
+    const int NQ = unoise_nq(n);
+    for (int qd = tid; qd < R * NQ * 64; qd += kNT) {   // drive √εU_k·gradU/2 + ξ (:1231)
+      const int l = qd / (NQ * 64), q = (qd >> 6) - l * NQ, lam = qd & 63;
+      double z[4];
+      normal_quad<4>(C.seed, (uint32_t)qd, (uint32_t)t, kUNoise, (uint32_t)k, z);
 #pragma unroll
-      for (int l = 0; l < R; l += 2) {
-        double z0, z1;
-        normal_pair(C.seed, (uint32_t)((l + RE * j) >> 1), (uint32_t)t, kUNoise, (uint32_t)k, z0, z1);
-        W_l[l * NS + j] = sk * W_l[l * NS + j] / 2 + z0;
-        if (l + 1 < R) W_l[(l + 1) * NS + j] = sk * W_l[(l + 1) * NS + j] / 2 + z1;
+      for (int i = 0; i < 4; ++i) {
+        const int j = lam + 64 * (4 * q + i);
+        if (j < n) W_l[l * NS + j] = sk * W_l[l * NS + j] / 2 + z[i];
       }
     }
   }
@@ -339,24 +342,21 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       gptr_w(C.U + (size_t)n * R * k)[o] = U_l[l * NS + j];
     }
     const uint32_t c3 = (uint32_t)(k + D * (2 * (blockIdx.y % P.ncls) + 1));
-    constexpr int RE = R + (R & 1);
-    for (int j = tid; j < n; j += kNT) {
+    const int NQ = unoise_nq(n);
+    for (int qd = tid; qd < R * NQ * 64; qd += kNT) {
+      const int l = qd / (NQ * 64), q = (qd >> 6) - l * NQ, lam = qd & 63;
+      double z[4] = {0.0, 0.0, 0.0, 0.0};
+      if (P.langevin) normal_quad<4>(C.seed, (uint32_t)qd, (uint32_t)t, kUNoise, c3, z);
 #pragma unroll
-      for (int l = 0; l < R; l += 2) {
-        double z0 = 0.0, z1 = 0.0;
-        if (P.langevin)
-          normal_pair(C.seed, (uint32_t)((l + RE * j) >> 1), (uint32_t)t, kUNoise, c3, z0, z1);
-        const double zz[2] = {z0, z1};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          if (l + h >= R) break;
-          const double G = gptr(C.gU)[(size_t)n * R * k + (size_t)n * (l + h) + j];
-          if (P.stiefel) {
-            W_l[(l + h) * NS + j] = sq * G / 2 + zz[h];
-          } else {
-            const double u = U_l[(l + h) * NS + j];
-            U_l[(l + h) * NS + j] = u + (C.epsU * (G - n * u) / 2 + sq * zz[h]);
-          }
+      for (int i = 0; i < 4; ++i) {
+        const int j = lam + 64 * (4 * q + i);
+        if (j >= n) break;
+        const double G = gptr(C.gU)[(size_t)n * R * k + (size_t)n * l + j];
+        if (P.stiefel) {
+          W_l[l * NS + j] = sq * G / 2 + z[i];
+        } else {
+          const double u = U_l[l * NS + j];
+          U_l[l * NS + j] = u + (C.epsU * (G - n * u) / 2 + sq * z[i]);
         }
       }
     }

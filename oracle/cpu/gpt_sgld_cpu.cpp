@@ -68,6 +68,27 @@ inline void normal_pair(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, ui
   z1 = rad * std::sin(th);
 }
 
+// U-noise contract (gpt_common.h normal_quad / oracle/philox.py unoise_quads): Philox block
+// c0 = (l·NQ + q)·64 + λ gives column l of rows λ + 64·(4q + i), i < 4, from 32-bit uniforms.
+inline double u32u(uint32_t x) { return ((double)x + 0.5) * (1.0 / 4294967296.0); }
+inline void unoise_quads(int n, int r, uint64_t seed, uint32_t c1, uint32_t c2, uint32_t c3,
+                         double* xi /* n×r column-major */) {
+  const int nq = ((n + 63) / 64 + 3) / 4;
+  for (int l = 0; l < r; ++l)
+    for (int q = 0; q < nq; ++q)
+      for (int lam = 0; lam < 64; ++lam) {
+        const U4 x = philox((uint32_t)((l * nq + q) * 64 + lam), c1, c2, c3, seed);
+        const double ra = std::sqrt(-2.0 * std::log(u32u(x.x)));
+        const double rb = std::sqrt(-2.0 * std::log(u32u(x.z)));
+        const double ta = 6.283185307179586 * u32u(x.y), tb = 6.283185307179586 * u32u(x.w);
+        const double z[4] = {ra * std::cos(ta), ra * std::sin(ta), rb * std::cos(tb), rb * std::sin(tb)};
+        for (int i = 0; i < 4; ++i) {
+          const int j = lam + 64 * (4 * q + i);
+          if (j < n) xi[j + (size_t)n * l] = z[i];
+        }
+      }
+}
+
 // ---------------------------------------------------------------- small dense helpers
 // Column-major n×c matrices.  C = A(m×k)·B(k×c)
 void matmul(int m, int k, int c, const double* A, const double* B, double* C) {
@@ -268,7 +289,6 @@ int run_chain(const Cfg& c, const double* phi, const double* y, const int32_t* I
   const long long nstore = (c.maxepoch * nb) / c.store_every;
   const long long total = c.max_steps > 0 ? std::min<long long>(c.max_steps, (c.burnin + c.maxepoch) * nb)
                                           : (c.burnin + c.maxepoch) * nb;
-  const int RE = r + (r & 1);
   std::vector<double> w(Q), U((size_t)n * r * D);
   init_state(n, r, D, Q, seed, c.sigma_w, w.data(), U.data());
   std::vector<int32_t> I0((size_t)Q * D);
@@ -349,14 +369,9 @@ int run_chain(const Cfg& c, const double* phi, const double* y, const int32_t* I
           }
         }
         double* Uk = U.data() + (size_t)n * r * k;
-        // drive = √εU·gradU/2 + ζ (:420), ζ[j,l] = element l + RE·j of (t, U_NOISE, k)
-        for (int j = 0; j < n; ++j)
-          for (int l = 0; l < r; l += 2) {
-            double z0, z1;
-            normal_pair(seed, (uint32_t)((l + RE * j) >> 1), (uint32_t)t, kUNoise, k, z0, z1);
-            mom[j + (size_t)n * l] = sq * (cU * gradU[j + (size_t)n * l]) / 2 + z0;
-            if (l + 1 < r) mom[j + (size_t)n * (l + 1)] = sq * (cU * gradU[j + (size_t)n * (l + 1)]) / 2 + z1;
-          }
+        // drive = √εU·gradU/2 + ζ (:420), ζ on the quad contract of (t, U_NOISE, k)
+        unoise_quads(n, r, seed, (uint32_t)t, kUNoise, (uint32_t)k, mom.data());
+        for (size_t e = 0; e < (size_t)n * r; ++e) mom[e] = sq * (cU * gradU[e]) / 2 + mom[e];
         // proj (:14-16): mom − U(Uᵀmom + momᵀU)/2
         for (int a = 0; a < r; ++a)
           for (int b = 0; b < r; ++b) {

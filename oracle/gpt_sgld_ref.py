@@ -306,11 +306,10 @@ def stiefel_init(Zr_n):
 
 
 def u_noise(n, r, seed, step, k):
-    """U-noise contract: ξ[j, l] = element l + RE·j of stream (step, U_NOISE, k), RE = r rounded
-    up to even (one Box–Muller pair serves columns (l, l+1) of a row).  Stands in for Julia's
-    ``randn(n, r)`` at GPT_SGLD.jl:420 / ``randn(n, r, D)`` at :426."""
-    re = r + (r & 1)
-    return px.normals(re * n, seed, step, px.U_NOISE, k).reshape((n, re))[:, :r]
+    """U-noise contract of stream (step, U_NOISE, k): the quad layout of ``philox.unoise_quads``
+    (one Philox block per four normals: column l of rows λ + 64·(4q + i)).  Stands in for
+    Julia's ``randn(n, r)`` at GPT_SGLD.jl:420 / ``randn(n, r, D)`` at :426."""
+    return px.unoise_quads(n, r, seed, step, px.U_NOISE, k)
 
 
 def init_state(n, r, D, Q, seed, stiefel=True, sigma_w=1.0):

@@ -15,8 +15,9 @@ reference one for one (SURVEY.md §8(a) "RNG consumption order"):
     U_INIT        (e>>1, 0,      U_INIT,  k)           Z = randn(r, n)       :365
     PERM          (i,    epoch,  PERM,    0)           randperm(N)           :373
     W_NOISE       (e>>1, step,   W_NOISE, 0)           randn(Q)              :412
-    U_NOISE       (e>>1, step,   U_NOISE, k)           randn(n, r)           :420
-                  element e = l + RE·j for ξ[j,l], RE = r rounded up to even
+    U_NOISE       (c0,   step,   U_NOISE, k)           randn(n, r)           :420
+                  quads: ξ[λ + 64(4q+i), l] for i < 4 from c0 = (l·NQ + q)·64 + λ,
+                  NQ = ceil(ceil(n/64)/4) (see ``unoise_quads``)
     THETA_INIT    (e>>1, 0,      TH_INIT, 0)           theta = randn(n)      :815
     THETA_NOISE   (e>>1, t,      TH_NOISE,0)           randn(n)              :836
 
@@ -91,6 +92,33 @@ def normals(count, seed, c1, c2, c3):
     z[0::2] = rad * np.cos(th)
     z[1::2] = rad * np.sin(th)
     return z[:count]
+
+
+def _u32(x):
+    """One uint32 word -> uniform double in (0, 1): (x + 1/2)·2^-32."""
+    return (x.astype(np.float64) + 0.5) * (1.0 / 4294967296.0)
+
+
+def unoise_quads(n, r, seed, c1, c2, c3):
+    """The n×r noise matrix of the U_NOISE contract (gpt_common.h normal_quad).  Rows come in
+    blocks of 64 (row j = λ + 64·b); Philox block c0 = (l·NQ + q)·64 + λ, NQ = ceil(ceil(n/64)/4),
+    gives column l of rows λ + 64·(4q + i), i = 0..3, as two Box–Muller pairs of 32-bit
+    uniforms u(x) = (x + 1/2)·2^-32: (z0, z1) = sqrt(-2 ln u(x0))·(cos 2πu(x1), sin 2πu(x1)) and
+    (z2, z3) from (x2, x3).  Rows >= n are dropped."""
+    n, r = int(n), int(r)
+    nq = (-(-n // 64) + 3) // 4
+    c0 = np.arange(r * nq * 64, dtype=np.uint32)
+    x0, x1, x2, x3 = philox4x32(c0, c1, c2, c3, seed)
+    ra = np.sqrt(-2.0 * np.log(_u32(x0)))
+    rb = np.sqrt(-2.0 * np.log(_u32(x2)))
+    ta, tb = 2.0 * np.pi * _u32(x1), 2.0 * np.pi * _u32(x3)
+    z = np.stack([ra * np.cos(ta), ra * np.sin(ta), rb * np.cos(tb), rb * np.sin(tb)])  # (4, cnt)
+    idx = np.arange(r * nq * 64)
+    l, q, lam = idx // (nq * 64), (idx // 64) % nq, idx % 64
+    out = np.empty((nq * 4 * 64, r))
+    for i in range(4):
+        out[lam + 64 * (4 * q + i), l] = z[i]
+    return out[:n]
 
 
 def uniform(seed, c1, c2, c3):
