@@ -281,7 +281,10 @@ extern "C" int gpt_device_count(void) {
   return c;
 }
 
-static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t_local) {
+// Steps t_local .. t_local+nsteps-1 of the sequence being enqueued (nsteps > 1 only on the chain
+// engine, within one epoch: every other kernel is one step per launch).
+static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t_local,
+                                 int nsteps = 1) {
   if (P.ncls)
     return launch_step_cls(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
                            t_local, s->stream);
@@ -293,7 +296,7 @@ static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t
                            t_local, s->stream);
   if (s->engine == kEngineChain)
     return launch_chain(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
-                        t_local, s->stream);
+                        t_local, nsteps, s->stream);
   return launch_step(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
                      t_local, s->stream);
 }
@@ -318,13 +321,22 @@ static hipError_t session_epoch_order(gpt_sgld_session* s, long long t_host, int
                             s->ord_ws.as<int32_t>(), s->stream);
 }
 
+// Steps of one epoch at most that one launch runs from host step t_host (chain engine: the rest of
+// the epoch within `left`; other engines: 1).
+static int session_span(const gpt_sgld_session* s, long long t_host, long long left) {
+  if (s->engine != kEngineChain || s->P.rms || s->P.wonly || s->P.ncls) return 1;
+  return (int)std::min<long long>(left, s->P.nb - t_host % s->P.nb);
+}
+
 static int session_enqueue(gpt_sgld_session* s, int count) {
   s->ran = true;
-  for (int i = 0; i < count; ++i) {
+  for (int i = 0; i < count;) {
     hipError_t e = session_epoch_order(s, s->steps_done + i, i);
     if (e != hipSuccess) return hip_fail(e, "launch_epoch_order");
-    e = session_launch(s, s->P, i);
+    const int span = session_span(s, s->steps_done + i, count - i);
+    e = session_launch(s, s->P, i, span);
     if (e != hipSuccess) return hip_fail(e, "launch_step");
+    i += span;
   }
   hipError_t e = launch_advance(s->tbase.as<long long>(), count, s->stream);
   if (e != hipSuccess) return hip_fail(e, "launch_advance");
@@ -596,13 +608,17 @@ extern "C" int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, 
   for (auto& e : ev) HIPCHK(hipEventCreate(&e));
   int rc = GPT_OK;
   s->ran = true;
-  for (long long i = 0; i < cnt && rc == GPT_OK; ++i) {
+  // one event pair per launch (a launch runs `span` steps on the chain engine)
+  long long nl = 0;
+  for (long long i = 0; i < cnt && rc == GPT_OK; ++nl) {
     hipError_t eo = session_epoch_order(s, s->steps_done + i, (int)i);   // outside the event pair
     if (eo != hipSuccess) return hip_fail(eo, "launch_epoch_order");
-    HIPCHK(hipEventRecord(ev[2 * i], s->stream));
-    hipError_t e = session_launch(s, s->P, (int)i);
+    const int span = session_span(s, s->steps_done + i, cnt - i);
+    HIPCHK(hipEventRecord(ev[2 * nl], s->stream));
+    hipError_t e = session_launch(s, s->P, (int)i, span);
     if (e != hipSuccess) rc = hip_fail(e, "launch_step");
-    HIPCHK(hipEventRecord(ev[2 * i + 1], s->stream));
+    HIPCHK(hipEventRecord(ev[2 * nl + 1], s->stream));
+    i += span;
   }
   if (rc == GPT_OK) {
     hipError_t e = launch_advance(s->tbase.as<long long>(), cnt, s->stream);
@@ -610,7 +626,7 @@ extern "C" int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, 
   }
   HIPCHK(hipStreamSynchronize(s->stream));
   double tot = 0.0;
-  for (long long i = 0; i < cnt; ++i) {
+  for (long long i = 0; i < nl; ++i) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
     tot += ms;

@@ -110,7 +110,7 @@ template <int R, int J, int G, int WV>
 __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepParams P,
                                                                 const ChainDesc* chains,
                                                                 const long long* __restrict__ tbase,
-                                                                int t_local) {
+                                                                int t_local, int nsteps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) double pbuf[kChainBufs * WV * G * 64 * J];   // row staging
   // Chain fields are read through Cp at their point of use (scalar loads) rather than held in
@@ -135,16 +135,25 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   double* pw0 = pbuf + k * (kChainBufs * G * 64 * J);           // this wave's staged rows
   double* bscr = wVr + G * kChainQS + k * G * R * kChainRunS;   // per row
 
-  const long long t = tbase[0] + t_local;
-  if (t >= P.total_steps) return;
+  // steps t0 .. tend-1 of this chain in one launch (a chunk of at most one epoch): U^(k) stays in
+  // registers and w in LDS between steps; the next batch's rows and targets are fetched during
+  // the previous step's Stiefel phase
+  const long long t0 = tbase[0] + t_local;
+  if (t0 >= P.total_steps) return;
   if (__hip_atomic_load(Cp->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   CSTAMP(0);
   if (CHAIN_PRIO && k >= 4) __builtin_amdgcn_s_setprio(1);
+  const long long tend = min(P.total_steps, t0 + (long long)nsteps);
 
-  const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
-  const int start = b * m;
-  const int Bt = min(m, P.N - start);
-  const int32_t* ord = Cp->order + (size_t)(e & 1) * P.N + start;
+  // batch of step tt: its rows of the epoch order and its length
+  auto batch_of = [&](long long tt, int& bt) -> const int32_t* {
+    const int ee = (int)(tt / P.nb), bb = (int)(tt - (long long)ee * P.nb);
+    bt = min(m, P.N - bb * m);
+    return Cp->order + (size_t)(ee & 1) * P.N + (size_t)bb * m;
+  };
+  long long t = t0;
+  int Bt;
+  const int32_t* ord = batch_of(t, Bt);
   const long long koff = (long long)n * k, rstride = (long long)n * D;
   const double* phi_k = uni_ptr(Cp->phi) + koff;
   // Stage rows g0n .. g0n+G-1 of this wave's dimension into pw (lane-linear LDS image: double j
@@ -206,7 +215,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     }
     for (int o = tid; o < kChainQPL * G; o += NTH) fp_l[o] = 0.0;
   }
-  for (int q = tid; q < Q; q += NTH) w_l[q] = gptr(Cp->w)[(size_t)(t & 1) * Q + q];
+  for (int q = tid; q < Q; q += NTH) w_l[q] = gptr(Cp->w)[(size_t)(t0 & 1) * Q + q];
   if (tid == 0) flag[0] = 0;
   {
     const double* yv = Cp->y;
@@ -235,16 +244,15 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 
 
 
-  double acc[J][R];
-#pragma unroll
-  for (int jj = 0; jj < J; ++jj)
-#pragma unroll
-    for (int l = 0; l < R; ++l) acc[jj][l] = 0.0;
   constexpr int TPW = (J >= 8 && WV > 4) ? 1 : kChainTasks;   // one task per wave at J = 8, D > 4
-  double vsave[TPW], gw[TPW];
-#pragma unroll
-  for (int x = 0; x < TPW; ++x) { vsave[x] = 0.0; gw[x] = 0.0; }
-
+  for (;;) {                             // ---------------------------------- one SGLD step
+  // thread ids the compiler cannot see through: per-lane addresses are formed inside the step
+  // instead of being hoisted out of the step loop and held in registers across it
+  int tid_o = threadIdx.x;
+  asm volatile("" : "+v"(tid_o));
+  const int tid = tid_o, lane = tid_o & 63;
+  for (int o = tid; o < G; o += NTH) wVr[o * kChainQS + kChainQP] = 0.0;   // gather zero slots
+  // (re-derived every step rather than held across the Stiefel phase, where registers are short)
   // this wave's V-task temp indices (< 256, four per register), fixed for the step
   unsigned itp[TPW][kChainDMax / 4];
 #pragma unroll
@@ -270,6 +278,15 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     for (int i = 0; i < 4; ++i)
       gq[i] = (unsigned)gptr(rq)[16 * i] | ((unsigned)gptr(rq)[16 * i + 8] << 16);
   }
+  double acc[J][R];
+#pragma unroll
+  for (int jj = 0; jj < J; ++jj)
+#pragma unroll
+    for (int l = 0; l < R; ++l) acc[jj][l] = 0.0;
+  double vsave[TPW], gw[TPW];
+#pragma unroll
+  for (int x = 0; x < TPW; ++x) { vsave[x] = 0.0; gw[x] = 0.0; }
+
   int slot = 0;
   for (int g0 = 0; g0 < Bt; g0 += G, slot ^= 1) {
     // lane id the compiler cannot see through: per-lane addresses are recomputed inside the
@@ -416,7 +433,11 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   }
   CSTAMP(2);
 
-  const ChainDesc C = *Cp;                 // loaded after the batch loop (see Cp)
+  // loaded after the batch loop (see Cp), through a pointer the compiler cannot see through, so
+  // that the load is not hoisted out of the step loop (the fields would then hold ~40 SGPRs)
+  const ChainDesc* Cq = Cp;
+  asm volatile("" : "+s"(Cq));
+  const ChainDesc C = *Cq;
   const double cN = (double)P.N / (double)Bt;
   const long long post = t - P.burnin_steps;
   const bool store = post >= 0 && ((post + 1) % P.store_every) == 0;
@@ -444,7 +465,8 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       double step = C.epsw * gradw / 2;
       step += sqe * normal_at(C.seed, (uint32_t)q, (uint32_t)t, kWNoise, 0);
       const double wn = wq + step;
-      gptr_w(C.w)[(size_t)((t + 1) & 1) * Q + q] = wn;
+      w_l[q] = wn;
+      if (t + 1 == tend) gptr_w(C.w)[(size_t)((t + 1) & 1) * Q + q] = wn;
       if (store && C.w_store) gptr_w(C.w_store)[(size_t)slot_s * Q + q] = wn;
       gn2 = fma(gradw, gradw, gn2);
     }
@@ -452,6 +474,21 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       gn2 = wave_sum(gn2);
       if (lane == 0) misc[k] = gn2;
     }
+  }
+  int Bn = 0;
+  const int32_t* ordn = nullptr;
+  if (t + 1 < tend) {
+    // every wave is past the batch loop: the next batch's indices, targets and first rows
+    ordn = batch_of(t + 1, Bn);
+    for (int i = tid; i < Bn; i += NTH) {
+      const int row = gptr(ordn)[i];
+      idx_l[i] = row;
+      y_l[i] = gptr(Cp->y)[row];
+    }
+    int rows0[G];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) rows0[gg] = gptr(ordn)[min(gg, Bn - 1)];
+    stage_rows(rows0, lane, pw0);
   }
   CSTAMP(3);
 
@@ -644,7 +681,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       if (tid == 0) __hip_atomic_store(C.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
-    double* Uk = C.U + (size_t)n * R * k;
+    double* Uk = (t + 1 == tend) ? C.U + (size_t)n * R * k : nullptr;
     double* Us = (store && C.U_store) ? C.U_store + ((size_t)slot_s * D + k) * n * R : nullptr;
 #pragma unroll
     for (int jj = 0; jj < J; ++jj) {
@@ -652,11 +689,15 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       if (j < n)
 #pragma unroll
         for (int l = 0; l < R; ++l) {
-          gptr_w(Uk)[j + (size_t)n * l] = u[jj][l];
+          if (Uk) gptr_w(Uk)[j + (size_t)n * l] = u[jj][l];
           if (Us) gptr_w(Us)[j + (size_t)n * l] = u[jj][l];
         }
     }
     CSTAMP(7);
+    if (++t >= tend) break;
+    ord = ordn;
+    Bt = Bn;
+  }
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -695,7 +736,7 @@ bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stie
 }
 
 hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchains,
-                        const long long* tbase, int t_local, hipStream_t st) {
+                        const long long* tbase, int t_local, int nsteps, hipStream_t st) {
   const int J = chain_J(P.n);
   const size_t lds = chain_lds_bytes(P.n, P.D, P.r, P.Q, P.m);
   dim3 grid(nchains), block(64 * P.D);
@@ -706,7 +747,7 @@ hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchain
                                     (int)(160 * 1024 - chain_static_lds(JJ, WW)), attr);      \
     if (e != hipSuccess) return e;                                                            \
     hipLaunchKernelGGL((chain_kernel<RR, JJ, kChainG, WW>), grid, block, lds, st, P, chains, tbase, \
-                       t_local);                                                              \
+                       t_local, nsteps);                                                      \
     return hipGetLastError();                                                                 \
   }
 #define CASE(RR, JJ) CASE_W(RR, JJ, kChainDMax) CASE_W(RR, JJ, 4)

@@ -165,8 +165,9 @@ bool rank_supported(int r);
 bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stiefel,
                      int max_run = 0);
 size_t chain_lds_bytes(int n, int D, int r, int Q, int m);
+// nsteps consecutive steps per launch (steps t .. t+nsteps-1 of one epoch at most)
 hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchains,
-                        const long long* tbase, int t_local, hipStream_t st);
+                        const long long* tbase, int t_local, int nsteps, hipStream_t st);
 
 
 hipError_t launch_pred_x(const double* w, const double* U, const int32_t* I0, const double* X,
