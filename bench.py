@@ -407,7 +407,12 @@ def main():
                          "traffic_source": traffic_src,
                          "kernel": ("chain_kernel<%d,J,2>" if info["engine"] == "chain"
                                     else "sgld_step_kernel<%d>") % r, "kernel_us": k_us,
-                         "algorithmic_bytes_per_launch": bytes_launch},
+                         "kernel_us_note": "per step of all chains; the chain engine runs up to "
+                                           "one epoch of steps per launch (one event pair per "
+                                           "launch, total / steps)",
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "algorithmic_bytes_per_step": bytes_launch,
+                         "steps_run_per_chain": sess.total_steps},
             "cpu_baseline": cpu,
             "test_rmse": quality["test_rmse"],
             "test_rmse_note": quality["note"],

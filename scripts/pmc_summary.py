@@ -43,6 +43,15 @@ def timed_launches(path, match):
     return g, by[g]
 
 
+def steps_run(log):
+    """Chain-steps per chain the profiled bench process ran (its JSON line), or None."""
+    try:
+        last = [l for l in open(log) if l.startswith("{")][-1]
+        return json.loads(last)["roofline"].get("steps_run_per_chain")
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("outdir")
@@ -70,6 +79,18 @@ def main():
     write = per_dispatch(os.path.join(args.outdir, "write", "run_counter_collection.csv"),
                          "WRITE_SIZE", args.kernel, grid)
     fm, wm = statistics.median(fetch), statistics.median(write)
+    # the chain engine runs up to one epoch of steps per launch: per-step figures are the sums
+    # over every launch of the kernel divided by the steps the process ran
+    ns = steps_run(os.path.join(args.outdir, "stats.log"))
+    nf = steps_run(os.path.join(args.outdir, "fetch.log"))
+    nw = steps_run(os.path.join(args.outdir, "write.log"))
+    per_step = {}
+    if ns and nf and nw:
+        per_step = {
+            "steps_run": ns,
+            "avg_duration_us_per_step": sum(durs) / ns,
+            "hbm_bytes_per_step": (2 * sum(fetch) / nf + sum(write) / nw) * 1024.0,
+        }
     entry = {
         "kernel": name.split("(")[0].replace("void ", ""),
         "avg_duration_us_all_launches": avg_ns / 1000.0,
@@ -82,7 +103,8 @@ def main():
         "launches": len(fetch),
         "correction": "gfx950 FETCH_SIZE counts half the bytes of 16-B/lane streaming reads "
                       "(MI355X_MICROARCH.md HBM): bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024",
-        "hbm_bytes_per_launch": (2 * fm + wm) * 1024.0,
+        "hbm_bytes_per_launch": per_step.get("hbm_bytes_per_step", (2 * fm + wm) * 1024.0),
+        "per_step": per_step,
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, separate passes "
                   "(scripts/profile_round.sh), tag %s" % args.tag,
     }
