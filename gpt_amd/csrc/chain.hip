@@ -29,6 +29,12 @@ namespace gpt {
 #ifndef CHAIN_PRIO                // s_setprio 1 for the second-dispatched half of the waves
 #define CHAIN_PRIO 0
 #endif
+#ifndef CHAIN_SPRIO               // Stiefel-phase priority of waves 4-7: 1 for the noise, 2 whole phase
+#define CHAIN_SPRIO 0
+#endif
+#ifndef CHAIN_TOUCH               // next-batch rows pulled into L2 / Infinity Cache during the
+#define CHAIN_TOUCH 0             // Stiefel phase (rows per dimension; 0 = off)
+#endif
 #ifndef CHAIN_STAGE_AT
 #define CHAIN_STAGE_AT 3          // next group's rows staged at: 0 (a), 1 (c), 2 (e), 3 end of (b), 4 end of (c)
 #endif
@@ -71,7 +77,8 @@ struct ChainLds {
   static constexpr int o_fp = al16c(o_temp + 8 * 2 * TS);
   static constexpr int o_gwp = al16c(o_fp + 8 * kChainQPL * G);
   static constexpr int o_misc = al16c(o_gwp + 8 * NTMAX * 64);
-  static constexpr int o_un = al16c(o_misc + 8 * 16);
+  static constexpr int o_touch = al16c(o_misc + 8 * 16);                // 256 B DMA sink
+  static constexpr int o_un = al16c(o_touch + 256);
   // union: w·V rows [row][q] (stride kChainQS) + per-wave reduction scratch (batch loop) |
   // per-wave post-batch scratch
   // (per-wave parts sized for the WV waves of the build: at WV = 4 the carve plus the row staging
@@ -95,6 +102,18 @@ struct ChainLds {
     if (P.stamps && g0 == 20 && lane == 0 && (k == 0 || k == 4))                            \
       P.stamps[(size_t)(gridDim.x + blockIdx.x) * kStamps + (k ? 8 : 0) + (slot)] =         \
           (long long)__builtin_amdgcn_s_memtime();                                         \
+  } while (0)
+
+// Stiefel sub-phase stamps (diagnostic runs only): waves 0 and 4 of every step, slot i < 16 in
+// stamp row (2 + i/8)·gridDim.x + blockIdx.x (columns i%8, +8 for wave 4).
+#ifndef CHAIN_SSTAMP
+#define CHAIN_SSTAMP 0            // diagnostic builds only (make diag): Stiefel sub-phase stamps
+#endif
+#define SSTAMP(slot)                                                                        \
+  do {                                                                                      \
+    if (CHAIN_SSTAMP && P.stamps && lane == 0 && (k == 0 || k == 4))                                        \
+      P.stamps[(size_t)((2 + (slot) / 8) * gridDim.x + blockIdx.x) * kStamps + (k ? 8 : 0) + \
+               (slot) % 8] = (long long)__builtin_amdgcn_s_memtime();                       \
   } while (0)
 
 // Workgroup barrier that orders LDS only: an LDS-DMA prefetch stays in flight across it
@@ -450,7 +469,9 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     if (task >= NT) break;
     gwp_l[task * 64 + lane] = gw[x];
   }
+  SSTAMP(0);
   __syncthreads();
+  SSTAMP(1);
   {
     const double inv_sw2 = 1.0 / (C.sigma_w * C.sigma_w);
     const double sqe = sqrt(C.epsw);
@@ -475,6 +496,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       if (lane == 0) misc[k] = gn2;
     }
   }
+  SSTAMP(2);
   int Bn = 0;
   const int32_t* ordn = nullptr;
   if (t + 1 < tend) {
@@ -489,10 +511,26 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) rows0[gg] = gptr(ordn)[min(gg, Bn - 1)];
     stage_rows(rows0, lane, pw0);
+    if constexpr (CHAIN_TOUCH > 0) {
+      // one 4-B piece per 128-B line of the next batch's first rows (lanes 0..31 span a 4-KB
+      // row slice): the lines land in L2 / the Infinity Cache while HBM is otherwise idle; the
+      // bytes go to a sink in LDS that nothing reads
+      __attribute__((address_space(3))) void* sink =
+          (__attribute__((address_space(3))) void*)(smem + L::o_touch);
+      const unsigned o = min(128u * (unsigned)(lane & 31), 8u * n - 4u);
+      for (int i = 0; i < CHAIN_TOUCH; ++i) {
+        const int row = gptr(ordn)[min(G + i, Bn - 1)];
+        const char* rb = (const char*)(phi_k + (long long)row * rstride);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(rb + o),
+                                         sink, 4, 0, 0);
+      }
+    }
   }
   CSTAMP(3);
+  SSTAMP(3);
 
   // ---- U^(k): gradient, Langevin drive, Stiefel projection + geodesic (per wave)
+  if (CHAIN_SPRIO && k >= 4) __builtin_amdgcn_s_setprio(1);
   const double cU = cN / C.signal_var;
   const double sq = sqrt(C.epsU);
   double gu2 = 0.0;
@@ -533,7 +571,9 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     gu2 = wave_sum(gu2);
     if (lane == 0) C.diag[(size_t)t * (1 + D) + 1 + k] = sqrt(gu2);
   }
+  if (CHAIN_SPRIO == 1) __builtin_amdgcn_s_setprio(0);
   CSTAMP(4);
+  SSTAMP(4);
   {
     constexpr int NN = 2 * R;
     constexpr int S0 = (7 * NN * NN > 64 * 8) ? 7 * NN * NN : 64 * 8;
@@ -558,6 +598,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       wave_sum_to_lds<R>(v, Mg + a * R);
     }
     wave_sync();
+    SSTAMP(5);
 #pragma unroll
     for (int bb = 0; bb < R; ++bb) {
       double ms[R];
@@ -590,6 +631,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       }
       wave_sync();
       CSTAMP(5);
+      SSTAMP(6);
       const double tt = sq;
       for (int o = lane; o < NN * NN; o += 64) {
         const int i = o / NN, j = o - i * NN;
@@ -599,7 +641,10 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         X0[o] = tt * v;
       }
       wave_sync();
-      const bool bad = wave_expm<NN>(X0);
+      long long* xst = (CHAIN_SSTAMP && P.stamps && k == 0)
+                           ? P.stamps + (size_t)(4 * gridDim.x + blockIdx.x) * kStamps : nullptr;
+      const bool bad = wave_expm<NN>(X0, xst);
+      SSTAMP(7);
       for (int o = lane; o < NN * R; o += 64) {
         const int a = o / R, l = o - a * R;
         Ec[o] = X0[NN * NN + a * NN + l];
@@ -608,9 +653,10 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       double* X1 = X0;                        // expm(−tA) in the same scratch
       for (int o = lane; o < R * R; o += 64) X1[o] = -tt * Ag[o];
       wave_sync();
-      wave_expm<R>(X1);
+      wave_expm<R>(X1, xst ? xst + (size_t)gridDim.x * kStamps : nullptr);
       if (bad && lane == 0) flag[0] = 1;
       CSTAMP(6);
+      SSTAMP(8);
       const double* mx = X1 + R * R;          // expm(−tA)
       // F = E[:,1:r]·expm(−tA) (NN × R, on the wave), then tmpU = [U mom]·F row by row
       // (GPT_SGLD.jl:35 with the two products associated the other way), then normalisation
@@ -624,6 +670,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         F[o] = s;
       }
       wave_sync();
+      SSTAMP(9);
       // two passes with R×R halves of F in registers: U·F[0:r,:] in place, then += mom·F[r:2r,:]
       // (each F value read from LDS once per wave)
       {
@@ -643,6 +690,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
           for (int l = 0; l < R; ++l) u[jj][l] = o[l];
         }
       }
+      SSTAMP(10);
       double nrm[R];
 #pragma unroll
       for (int l = 0; l < R; ++l) nrm[l] = 0.0;
@@ -660,8 +708,10 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
           for (int l = 0; l < R; ++l) nrm[l] = fma(u[jj][l], u[jj][l], nrm[l]);
         }
       }
+      SSTAMP(11);
       wave_sum_to_lds<R>(nrm, nr);
       wave_sync();
+      SSTAMP(12);
 #pragma unroll
       for (int l = 0; l < R; ++l) {
         const double isc = 1.0 / sqrt(nr[l]);
@@ -669,8 +719,10 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         for (int jj = 0; jj < J; ++jj) u[jj][l] = u[jj][l] * isc;
       }
     }
+    SSTAMP(13);
     if (P.stamps && lane == 0)            // per-wave arrival at the end-of-step barrier (diag)
     P.stamps[(size_t)blockIdx.x * kStamps + 8 + k] = (long long)__builtin_amdgcn_s_memtime();
+  if (CHAIN_SPRIO == 2) __builtin_amdgcn_s_setprio(0);
   __syncthreads();                      // w_l, flag and the gradw partials are complete
     if (C.diag && tid == 0) {
       double s = 0.0;
@@ -694,6 +746,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         }
     }
     CSTAMP(7);
+    SSTAMP(15);
     if (++t >= tend) break;
     ord = ordn;
     Bt = Bn;

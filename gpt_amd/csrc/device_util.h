@@ -621,6 +621,7 @@ __device__ bool wave_expm(double* S, long long* st = nullptr) {
   int si = 0;
   if (nA <= 2.1) {
     const int deg = nA > 0.95 ? 9 : (nA > 0.25 ? 7 : (nA > 0.015 ? 5 : 3));
+    if (st && lane == 0) st[10] = deg;
     const double* C = kPade[(deg - 3) / 2];   // wave-uniform: scalar loads from constant memory
     wave_mm<NN>(A, A, A2);
     const double c0 = C[0], c1 = C[1];
@@ -650,6 +651,7 @@ __device__ bool wave_expm(double* S, long long* st = nullptr) {
     const double s = log2(nA / 5.4);
     si = (s > 0.0) ? (s < 60.0 ? (int)ceil(s) : 60) : 0;
     if (!(nA == nA)) si = 0;
+    if (st && lane == 0) st[10] = 13 + 100 * si;
     if (si > 0) {
       const double sc = ldexp(1.0, -si);
       for (int o = lane; o < q; o += 64) A[o] *= sc;

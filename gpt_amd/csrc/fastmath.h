@@ -3,7 +3,8 @@
 // The library versions carry Payne–Hanek reduction tables and long polynomial ladders whose
 // constants the compiler hoists into registers next to the kernels' resident U / gradU tiles.
 // Box–Muller only needs log on (0, 1] and sin/cos of 2πu with u in (0, 1), so:
-//   log: fdlibm's e_log.c scheme (s = f/(2+f), degree-14 minimax in s) — error < 1 ulp;
+//   log: fdlibm's e_log.c scheme (s = f/(2+f), degree-14 minimax in s; on the device the
+//        quotient is f times a Newton-refined reciprocal) — error < 2 ulp;
 //   sincos(2πu): exact quadrant reduction on 4u (no π rounding in the reduction), then
 //        fdlibm's __kernel_sin / __kernel_cos on |φ| <= π/4 — error < 1 ulp.
 // Results can differ from glibc (the oracle's numpy) in the last bit; parity tolerances cover it.
@@ -32,6 +33,19 @@ namespace gpt {
    -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11,         \
    1.57079632679489655800e+00, 6.12323399573676603587e-17}
 
+// 1/x: on the device the hardware reciprocal plus two Newton steps (within 1 ulp)
+GPT_HD double fm_rcp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(GPT_FM_OLD)
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+#else
+  return 1.0 / x;
+#endif
+}
+
 template <class CP>
 GPT_HD double fm_log_c(double x, CP c) {   // x in (0, +inf), finite
   uint64_t bits;
@@ -42,7 +56,7 @@ GPT_HD double fm_log_c(double x, CP c) {   // x in (0, +inf), finite
   memcpy(&mnt, &mb, 8);
   if (mnt > 1.4142135623730951) { mnt *= 0.5; e += 1; }                  // [√½, √2)
   const double f = mnt - 1.0;
-  const double s = f / (2.0 + f);
+  const double s = f * fm_rcp(2.0 + f);
   const double z = s * s, w = z * z;
   const double t1 = w * (c[1] + w * (c[3] + w * c[5]));
   const double t2 = z * (c[0] + w * (c[2] + w * (c[4] + w * c[6])));
@@ -68,12 +82,36 @@ GPT_HD void fm_sincos_2pi_c(double u, double& sn, double& cs, CP c) {
   const double hz = 0.5 * z;
   const double w = 1.0 - hz;
   const double cc = w + (((1.0 - w) - hz) + z * rc);
-  switch (q) {
-    case 0: sn = s; cs = cc; break;
-    case 1: sn = cc; cs = -s; break;
-    case 2: sn = -s; cs = -cc; break;
-    default: sn = -cc; cs = s; break;
-  }
+  // quadrant q: (sin, cos) = (s, cc), (cc, −s), (−s, −cc), (−cc, s) — selects and sign-bit flips
+  // (no divergent branches, so the independent Box–Muller chains of a caller interleave)
+  const bool odd = (q & 1) != 0;
+  uint64_t bs, bc;
+  const double s0 = odd ? cc : s, c0 = odd ? s : cc;
+  memcpy(&bs, &s0, 8);
+  memcpy(&bc, &c0, 8);
+  bs ^= (uint64_t)((q >> 1) & 1) << 63;
+  bc ^= (uint64_t)(((q + 1) >> 1) & 1) << 63;
+  memcpy(&sn, &bs, 8);
+  memcpy(&cs, &bc, 8);
+}
+
+// √x for finite normal x > 0 (the Box–Muller radius: x = −2 ln u in [2e-10, 46]): on the device
+// the hardware rsq refined by two Newton steps (the refinement of the library expansion without
+// its denormal scaling and class checks).
+GPT_HD double fm_sqrt_pos(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(GPT_FM_OLD)
+  double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  return fma(d, h, g);
+#else
+  return sqrt(x);
+#endif
 }
 
 struct FmHostCoef {

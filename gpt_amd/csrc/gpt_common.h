@@ -60,7 +60,7 @@ __device__ __forceinline__ double normal_at(uint64_t seed, uint32_t e, uint32_t 
   const U4 x = philox4x32(e >> 1, c1, c2, c3, seed);
   const double u1 = u53(x.x, x.y), u2 = u53(x.z, x.w);
   const auto c = fm_coef();
-  const double rad = sqrt(-2.0 * fm_log_c(u1, c));
+  const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u1, c));
   double sn, cs;
   fm_sincos_2pi_c(u2, sn, cs, c);
   return (e & 1u) ? rad * sn : rad * cs;
@@ -72,7 +72,7 @@ __device__ __forceinline__ void normal_pair(uint64_t seed, uint32_t c0, uint32_t
   const U4 x = philox4x32(c0, c1, c2, c3, seed);
   const double u1 = u53(x.x, x.y), u2 = u53(x.z, x.w);
   const auto c = fm_coef();
-  const double rad = sqrt(-2.0 * fm_log_c(u1, c));
+  const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u1, c));
   double sn, cs;
   fm_sincos_2pi_c(u2, sn, cs, c);
   z0 = rad * cs;
@@ -97,14 +97,14 @@ __device__ __forceinline__ void normal_quad(uint64_t seed, uint32_t c0, uint32_t
   const U4 x = philox4x32(c0, c1, c2, c3, seed);
   const auto c = fm_coef();
   {
-    const double rad = sqrt(-2.0 * fm_log_c(u32u(x.x), c));
+    const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.x), c));
     double sn, cs;
     fm_sincos_2pi_c(u32u(x.y), sn, cs, c);
     z[0] = rad * cs;
     z[1] = rad * sn;
   }
   if constexpr (NZ == 4) {
-    const double rad = sqrt(-2.0 * fm_log_c(u32u(x.z), c));
+    const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.z), c));
     double sn, cs;
     fm_sincos_2pi_c(u32u(x.w), sn, cs, c);
     z[2] = rad * cs;

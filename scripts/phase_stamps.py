@@ -55,6 +55,7 @@ def main():
         # workgroup c writes slot c of it
         out = np.zeros((args.steps, (D + 1) * args.chains, 16), dtype=np.int64)
         check(lib().gpt_sgld_session_stamps(s._h, args.steps, out.ctypes.data_as(C.POINTER(C.c_int64))))
+        out_all = out
         lp = out[:, args.chains:2 * args.chains, :]
         out = out[:, :args.chains, :]
         tot = np.median((out[..., 7] - out[..., 0]).ravel())
@@ -78,6 +79,35 @@ def main():
                       + "  (total %d)" % np.median(lp[..., base + 7] - lp[..., base]))
             print("  wave 4 starts the group %d cycles after wave 0"
                   % np.median(lp[..., 8] - lp[..., 0]))
+        sp = np.concatenate([out_all[:, 2 * args.chains:3 * args.chains, :],
+                             out_all[:, 3 * args.chains:4 * args.chains, :]], axis=2)
+        # sp[..., 0:8] wave 0 slots 0-7, [8:16] wave 4 slots 0-7, [16:24] wave 0 slots 8-15,
+        # [24:32] wave 4 slots 8-15
+        if (sp[..., 0] > 0).all():
+            snames = ["", "gwp barrier", "w update", "next batch idx/y + DMA", "noise+drive",
+                      "proj", "geod grams", "expm 2r", "expm r", "F", "U.F pass", "mom.F pass + norms",
+                      "norm sums", "normalise", "(unused)", "end barrier + U write"][:16]
+            for wv, cols in (("wave 0", list(range(0, 8)) + list(range(16, 24))),
+                             ("wave 4", list(range(8, 16)) + list(range(24, 32)))):
+                ts = sp[..., cols]
+                parts = []
+                for i in range(1, 16):
+                    if i == 14 or not (ts[..., i] > 0).all():
+                        continue
+                    j = i - 1
+                    while j == 14 or not (ts[..., j] > 0).all():
+                        j -= 1
+                    parts.append("%s %d" % (snames[i], np.median(ts[..., i] - ts[..., j])))
+                print("  Stiefel phase, %s (cycles): %s" % (wv, ", ".join(parts)))
+                print("    %s: w-start %d cycles after wave 0's, end at +%d" % (
+                    wv, np.median(ts[..., 0] - sp[..., 0]), np.median(ts[..., 15] - ts[..., 0])))
+        for nm, row in (("expm 2r", 4), ("expm r", 5)):
+            xs = out_all[:, row * args.chains:(row + 1) * args.chains, :]
+            if (xs[..., 11:15] > 0).all():
+                dx = np.median((xs[..., 12:15] - xs[..., 11:14]).reshape(-1, 3), axis=0)
+                degs, cnt = np.unique(xs[..., 10], return_counts=True)
+                print("  %s (wave 0): products %d, solve %d, squarings %d cycles; degree/scaling %s"
+                      % ((nm,) + tuple(dx) + (dict(zip(degs.tolist(), cnt.tolist())),)))
         print("event-timed step kernel: %.2f us" % s.time_steps(20))
         return
     nb = (D + 1) * args.chains
