@@ -561,9 +561,13 @@ __device__ __forceinline__ bool wave_solve_dd(const double* M, double* X) {
     const int c = lane < NN ? lane : lane - NN;
     col[i] = lane < NN ? M[i * NN + c] : (lane < 2 * NN ? X[i * NN + c] : 0.0);
   }
+  // the reciprocal of each pivot (Newton-refined, within 1 ulp) scales both the multipliers and
+  // the back substitution: no division on the elimination's critical path
+  double rpv[NN];
 #pragma unroll
   for (int p = 0; p < NN; ++p) {              // forward elimination (getrf + L solve)
-    const double rp = 1.0 / readlane_d(col[p], p);
+    const double rp = rcp_nr(readlane_d(col[p], p));
+    rpv[p] = rp;
 #pragma unroll
     for (int i = p + 1; i < NN; ++i) {
       const double f = readlane_d(col[i], p) * rp;
@@ -575,9 +579,9 @@ __device__ __forceinline__ bool wave_solve_dd(const double* M, double* X) {
   for (int k = NN - 1; k >= 0; --k) {         // back substitution, column-oriented (trsm)
     double u[NN];
 #pragma unroll
-    for (int i = 0; i <= k; ++i) u[i] = readlane_d(col[i], k);   // U[0..k][k] from lane k
+    for (int i = 0; i < k; ++i) u[i] = readlane_d(col[i], k);    // U[0..k-1][k] from lane k
     if (xl) {
-      col[k] = col[k] / u[k];
+      col[k] = col[k] * rpv[k];
 #pragma unroll
       for (int i = 0; i < k; ++i) col[i] -= col[k] * u[i];
     }
