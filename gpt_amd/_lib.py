@@ -98,6 +98,25 @@ SIGNATURES = {
                                      C.c_int64, C.c_int64, C.c_int64, C.c_uint64, C.c_double,
                                      C.c_double, C.c_int32, C.c_int32, P_D, P_D, P_D, P_D, P_D,
                                      P_D]),
+    "gpt_cf_fixw_sideinfo": (C.c_int, [P_D, C.c_int64, C.c_int64, P_D, C.c_int64, C.c_int64, P_D,
+                                       C.c_int64, C.c_int64, P_D, C.c_int64, C.c_int64,
+                                       C.c_double, C.c_double, P_D, C.c_int64, C.c_int64,
+                                       C.c_double, C.c_double, C.c_double, C.c_double, C.c_int64,
+                                       C.c_int64, C.c_uint64, C.c_double, C.c_double, C.c_int32,
+                                       C.c_int32, C.c_int32, P_D, P_D, P_D, P_D, P_D]),
+    "gpt_cf_fullw": (C.c_int, [P_D, C.c_int64, C.c_int64, C.c_int64, C.c_int64, P_D, C.c_int64,
+                               C.c_int64, C.c_double, C.c_double, C.c_double, P_D, C.c_int64,
+                               C.c_int64, C.c_double, C.c_double, C.c_int64, C.c_int64,
+                               C.c_uint64, C.c_double, C.c_double, C.c_int32, C.c_int32,
+                               C.c_int32, P_D, P_D, P_D, P_D, P_D, P_D]),
+    "gpt_cf_fixw": (C.c_int, [P_D, C.c_int64, C.c_int64, C.c_int64, C.c_int64, P_D, C.c_int64,
+                              C.c_int64, C.c_double, C.c_double, P_D, C.c_int64, C.c_int64,
+                              C.c_double, C.c_int64, C.c_int64, C.c_uint64, C.c_double, C.c_double,
+                              C.c_int32, C.c_int32, C.c_int32, P_D, P_D, P_D, P_D, P_D]),
+    "gpt_cf_fixw_gibbs": (C.c_int, [P_D, C.c_int64, C.c_int64, C.c_int64, C.c_int64, P_D,
+                                    C.c_int64, C.c_int64, C.c_double, C.c_double, P_D, C.c_int64,
+                                    C.c_int64, C.c_int64, C.c_int64, C.c_uint64, C.c_double,
+                                    C.c_double, C.c_int32, C.c_int32, P_D, P_D, P_D, P_D, P_D]),
     "gpt_tgp_gibbs": (C.c_int, [P_D, P_D, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                 C.c_double, C.c_int64, C.c_int64, C.c_uint64, P_I32, P_D, P_D,
                                 P_I32]),

@@ -1372,22 +1372,33 @@ static void cf_features(const double* X, int n, int D, int rowbase, std::vector<
   if (fe.empty()) fe.push_back(0);
 }
 
-extern "C" int gpt_cf_fullw_sideinfo(
-    const double* Rating, int64_t N, int64_t ldr, const double* UserData, int64_t n1, int64_t D1,
-    const double* MovieData, int64_t n2, int64_t D2, const double* Ratingtest, int64_t Ntest,
-    int64_t ldt, double signal_var, double sigma_u, double sigma_w, const double* w_init, int64_t r,
-    int64_t m, double epsw, double epsU, double a, double b, double c, int64_t burnin,
-    int64_t maxepoch, uint64_t seed, double ytrainMean, double ytrainStd, int32_t langevin,
-    int32_t stiefel, int32_t avg, double* w_store, double* U_store, double* V_store,
-    double* testpred_store, double* trainRMSE, double* testRMSE) {
-  if (!Rating || !UserData || !MovieData || !Ratingtest || !w_init || !w_store || !U_store ||
+// U, V initialisation of the SGD / SGLD CF samplers (the reference's variants differ):
+//   kCfInitSide  GPT_fullw_sideinfo :424-428  stiefel ? polar(randn(r,rows)) : σ_u·randn(rows,r)
+//   kCfInitSigma GPT_fixw / GPT_fixw_sideinfo :67 / :294  σ_u·randn(rows,r) (also when stiefel)
+//   kCfInitUnit  GPT_fullw :175-180           stiefel ? polar(randn(r,rows)) : randn(rows,r)
+enum CfInit { kCfInitSide = 0, kCfInitSigma = 1, kCfInitUnit = 2 };
+
+// One SGD / SGLD run of the tensor CF model (the body of every GPT_*w* SGD variant): fixw keeps
+// w at w_init (w_store may then be null), D1 = D2 = 0 with a = 1, b = c = 0 is the model without
+// side information.
+static int cf_sgd_run(
+    const char* name, const double* Rating, int64_t N, int64_t ldr, const double* UserData,
+    int64_t n1, int64_t D1, const double* MovieData, int64_t n2, int64_t D2,
+    const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var, double sigma_u,
+    double sigma_w, const double* w_init, int64_t r, int64_t m, double epsw, double epsU, double a,
+    double b, double c, int64_t burnin, int64_t maxepoch, uint64_t seed, double ytrainMean,
+    double ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg, bool fixw, CfInit init,
+    double* w_store, double* U_store, double* V_store, double* testpred_store, double* trainRMSE,
+    double* testRMSE) {
+  if (!Rating || (D1 > 0 && !UserData) || (D2 > 0 && !MovieData) || !Ratingtest || !w_init ||
+      (!fixw && !w_store) || !U_store ||
       !V_store || !testpred_store || !trainRMSE || !testRMSE || N < 1 || Ntest < 1 || ldr < N ||
       ldt < Ntest || n1 < 1 || n2 < 1 || D1 < 0 || D2 < 0 || m < 1 || burnin < 0 || maxepoch < 0 ||
       !(signal_var > 0) || !(sigma_u > 0) || !(sigma_w > 0)) {
-    set_error("bad GPT_fullw_sideinfo arguments"); return GPT_ERR_BAD_DIMS;
+    set_error(std::string("bad ") + name + " arguments"); return GPT_ERR_BAD_DIMS;
   }
   if (!cf_rank_supported((int)r) || cf_lds_bytes((int)r, (int)m) > 160 * 1024) {
-    set_error("GPT_fullw_sideinfo: rank not instantiated (1-6,8,10,12,15,16,20) or minibatch too large");
+    set_error(std::string(name) + ": rank not instantiated (1-6,8,10,12,15,16,20) or minibatch too large");
     return GPT_ERR_BAD_DIMS;
   }
   const int rowsU = (int)(n1 + D1), rowsV = (int)(n2 + D2);
@@ -1411,7 +1422,8 @@ extern "C" int gpt_cf_fullw_sideinfo(
     double* M = which ? V0.data() : U0.data();
     std::vector<double> Z((size_t)rows * r);
     for (size_t e = 0; e < Z.size(); ++e) Z[e] = host_normal(seed, (uint32_t)e, 0, kCfUVInit, (uint32_t)which);
-    if (stiefel) host_stiefel_polar(Z.data(), (int)r, rows, M);
+    if (stiefel && init != kCfInitSigma) host_stiefel_polar(Z.data(), (int)r, rows, M);
+    else if (init == kCfInitUnit) for (size_t e = 0; e < Z.size(); ++e) M[e] = Z[e];
     else for (size_t e = 0; e < Z.size(); ++e) M[e] = sigma_u * Z[e];
   }
   const size_t nU = U0.size(), nV = V0.size(), rr = (size_t)r * r;
@@ -1448,6 +1460,7 @@ extern "C" int gpt_cf_fullw_sideinfo(
   P.rowsU = rowsU; P.rowsV = rowsV;
   P.a = a; P.b = b; P.c = c; P.signal_var = signal_var; P.sigma_u = sigma_u; P.sigma_w = sigma_w;
   P.epsw = epsw; P.epsU = epsU; P.langevin = langevin; P.stiefel = stiefel; P.seed = seed;
+  P.fixw = fixw ? 1 : 0;
   P.uptr = d_up.as<int32_t>(); P.ufe = d_uf.as<int32_t>(); P.vptr = d_vp.as<int32_t>(); P.vfe = d_vf.as<int32_t>();
   CfChain C{};
   C.tr_user = d_tu.as<int32_t>(); C.tr_movie = d_tm.as<int32_t>(); C.tr_rating = d_tr.as<double>();
@@ -1458,7 +1471,7 @@ extern "C" int gpt_cf_fullw_sideinfo(
   C.trainpred = d_trp.as<double>(); C.testpred = d_tep.as<double>(); C.sse = d_sse.as<double>();
   C.status = d_st.as<int32_t>();
   HIPCHK(hipMemcpy(d_ch.p, &C, sizeof(CfChain), hipMemcpyHostToDevice));
-  std::memset(w_store, 0, 8 * rr * maxepoch);
+  if (w_store) std::memset(w_store, 0, 8 * rr * maxepoch);
   std::memset(U_store, 0, 8 * nU * maxepoch);
   std::memset(V_store, 0, 8 * nV * maxepoch);
   std::memset(testpred_store, 0, 8 * (size_t)Ntest * maxepoch);
@@ -1475,7 +1488,7 @@ extern "C" int gpt_cf_fullw_sideinfo(
     int32_t bad = 0;
     HIPCHK(hipMemcpy(&bad, d_st.p, 4, hipMemcpyDeviceToHost));
     if (bad) {                       // :490-492 — zero parameter stores, curves as they are
-      std::memset(w_store, 0, 8 * rr * maxepoch);
+      if (w_store) std::memset(w_store, 0, 8 * rr * maxepoch);
       std::memset(U_store, 0, 8 * nU * maxepoch);
       std::memset(V_store, 0, 8 * nV * maxepoch);
       set_error("Get NaN when moving along Geodesic. Try smaller epsU");
@@ -1483,7 +1496,7 @@ extern "C" int gpt_cf_fullw_sideinfo(
     }
     if (epoch > burnin) {
       const int64_t s2 = epoch - burnin - 1;
-      HIPCHK(hipMemcpy(w_store + rr * s2, d_w.p, 8 * rr, hipMemcpyDeviceToHost));
+      if (w_store) HIPCHK(hipMemcpy(w_store + rr * s2, d_w.p, 8 * rr, hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(U_store + nU * s2, d_U.p, 8 * nU, hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(V_store + nV * s2, d_V.p, 8 * nV, hipMemcpyDeviceToHost));
       if (!avg) counter = 0;
@@ -1506,6 +1519,63 @@ extern "C" int gpt_cf_fullw_sideinfo(
     if (testcounter >= 5) break;
   }
   return GPT_OK;
+}
+
+extern "C" int gpt_cf_fullw_sideinfo(
+    const double* Rating, int64_t N, int64_t ldr, const double* UserData, int64_t n1, int64_t D1,
+    const double* MovieData, int64_t n2, int64_t D2, const double* Ratingtest, int64_t Ntest,
+    int64_t ldt, double signal_var, double sigma_u, double sigma_w, const double* w_init, int64_t r,
+    int64_t m, double epsw, double epsU, double a, double b, double c, int64_t burnin,
+    int64_t maxepoch, uint64_t seed, double ytrainMean, double ytrainStd, int32_t langevin,
+    int32_t stiefel, int32_t avg, double* w_store, double* U_store, double* V_store,
+    double* testpred_store, double* trainRMSE, double* testRMSE) {
+  return cf_sgd_run("GPT_fullw_sideinfo", Rating, N, ldr, UserData, n1, D1, MovieData, n2, D2,
+                    Ratingtest, Ntest, ldt, signal_var, sigma_u, sigma_w, w_init, r, m, epsw, epsU,
+                    a, b, c, burnin, maxepoch, seed, ytrainMean, ytrainStd, langevin, stiefel, avg,
+                    false, kCfInitSide, w_store, U_store, V_store, testpred_store, trainRMSE,
+                    testRMSE);
+}
+
+extern "C" int gpt_cf_fixw_sideinfo(
+    const double* Rating, int64_t N, int64_t ldr, const double* UserData, int64_t n1, int64_t D1,
+    const double* MovieData, int64_t n2, int64_t D2, const double* Ratingtest, int64_t Ntest,
+    int64_t ldt, double signal_var, double sigma_u, const double* w, int64_t r, int64_t m,
+    double epsU, double a, double b, double c, int64_t burnin, int64_t maxepoch, uint64_t seed,
+    double ytrainMean, double ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg,
+    double* U_store, double* V_store, double* testpred_store, double* trainRMSE,
+    double* testRMSE) {
+  return cf_sgd_run("GPT_fixw_sideinfo", Rating, N, ldr, UserData, n1, D1, MovieData, n2, D2,
+                    Ratingtest, Ntest, ldt, signal_var, sigma_u, 1.0, w, r, m, 0.0, epsU, a, b, c,
+                    burnin, maxepoch, seed, ytrainMean, ytrainStd, langevin, stiefel, avg, true,
+                    kCfInitSigma, nullptr, U_store, V_store, testpred_store, trainRMSE, testRMSE);
+}
+
+extern "C" int gpt_cf_fullw(const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2,
+                            const double* Ratingtest, int64_t Ntest, int64_t ldt,
+                            double signal_var, double sigma_u, double sigma_w,
+                            const double* w_init, int64_t r, int64_t m, double epsw, double epsU,
+                            int64_t burnin, int64_t maxepoch, uint64_t seed, double ytrainMean,
+                            double ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg,
+                            double* w_store, double* U_store, double* V_store,
+                            double* testpred_store, double* trainRMSE, double* testRMSE) {
+  return cf_sgd_run("GPT_fullw", Rating, N, ldr, nullptr, n1, 0, nullptr, n2, 0, Ratingtest,
+                    Ntest, ldt, signal_var, sigma_u, sigma_w, w_init, r, m, epsw, epsU, 1.0, 0.0,
+                    0.0, burnin, maxepoch, seed, ytrainMean, ytrainStd, langevin, stiefel, avg,
+                    false, kCfInitUnit, w_store, U_store, V_store, testpred_store, trainRMSE,
+                    testRMSE);
+}
+
+extern "C" int gpt_cf_fixw(const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2,
+                           const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var,
+                           double sigma_u, const double* w, int64_t r, int64_t m, double epsU,
+                           int64_t burnin, int64_t maxepoch, uint64_t seed, double ytrainMean,
+                           double ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg,
+                           double* U_store, double* V_store, double* testpred_store,
+                           double* trainRMSE, double* testRMSE) {
+  return cf_sgd_run("GPT_fixw", Rating, N, ldr, nullptr, n1, 0, nullptr, n2, 0, Ratingtest, Ntest,
+                    ldt, signal_var, sigma_u, 1.0, w, r, m, 0.0, epsU, 1.0, 0.0, 0.0, burnin,
+                    maxepoch, seed, ytrainMean, ytrainStd, langevin, stiefel, avg, true,
+                    kCfInitSigma, nullptr, U_store, V_store, testpred_store, trainRMSE, testRMSE);
 }
 
 // Q of a Householder QR (LAPACK dgeqr2 + dorg2r conventions), r × r column-major in place.
@@ -1543,21 +1613,23 @@ static void host_qr_q(int r, std::vector<double>& A) {
   A.swap(Qm);
 }
 
-extern "C" int gpt_cf_fullw_gibbs(
-    const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2, const double* Ratingtest,
-    int64_t Ntest, int64_t ldt, double signal_var, double sigma_u, double sigma_w,
-    const double* w_init, int64_t r, int64_t burnin, int64_t maxepoch, int64_t n_samples,
-    uint64_t seed, double ytrainMean, double ytrainStd, int32_t avg, int32_t rotated_w,
-    double* w_store, double* U_store, double* V_store, double* testpred_store, double* trainRMSE,
-    double* testRMSE) {
-  if (!Rating || !Ratingtest || !w_init || !w_store || !U_store || !V_store || !testpred_store ||
+// Gibbs sweeps of the CF model without side information (GPT_fullw_gibbs; fixw: GPT_fixw_gibbs,
+// :945-1028 — the same user / movie conditionals, no w draw, w_store may be null).
+static int cf_gibbs_run(
+    const char* name, const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2,
+    const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var, double sigma_u,
+    double sigma_w, const double* w_init, int64_t r, int64_t burnin, int64_t maxepoch,
+    int64_t n_samples, uint64_t seed, double ytrainMean, double ytrainStd, int32_t avg,
+    int32_t rotated_w, bool fixw, double* w_store, double* U_store, double* V_store,
+    double* testpred_store, double* trainRMSE, double* testRMSE) {
+  if (!Rating || !Ratingtest || !w_init || (!fixw && !w_store) || !U_store || !V_store || !testpred_store ||
       !trainRMSE || !testRMSE || N < 1 || Ntest < 1 || ldr < N || ldt < Ntest || n1 < 1 || n2 < 1 ||
       burnin < 0 || maxepoch < 0 || n_samples < 1 || !(signal_var > 0) || !(sigma_u > 0) ||
       !(sigma_w > 0)) {
-    set_error("bad GPT_fullw_gibbs arguments"); return GPT_ERR_BAD_DIMS;
+    set_error(std::string("bad ") + name + " arguments"); return GPT_ERR_BAD_DIMS;
   }
   if (!cf_rank_supported((int)r) || r * r > 1024) {
-    set_error("GPT_fullw_gibbs: rank not instantiated (1-6,8,10,12,15,16,20)"); return GPT_ERR_BAD_DIMS;
+    set_error(std::string(name) + ": rank not instantiated (1-6,8,10,12,15,16,20)"); return GPT_ERR_BAD_DIMS;
   }
   std::vector<int32_t> tu(N), tm(N), eu(Ntest), em(Ntest);
   std::vector<double> tr(N), er(Ntest);
@@ -1643,7 +1715,7 @@ extern "C" int gpt_cf_fullw_gibbs(
   Cc.V = d_V.as<double>(); Cc.trainpred = d_trp.as<double>(); Cc.testpred = d_tep.as<double>();
   Cc.sse = d_sse.as<double>(); Cc.status = d_st.as<int32_t>();
   HIPCHK(hipMemcpy(d_ch.p, &Cc, sizeof(CfChain), hipMemcpyHostToDevice));
-  std::memset(w_store, 0, 8 * rr * maxepoch);
+  if (w_store) std::memset(w_store, 0, 8 * rr * maxepoch);
   std::memset(U_store, 0, 8 * nU * maxepoch);
   std::memset(V_store, 0, 8 * nV * maxepoch);
   std::memset(testpred_store, 0, 8 * (size_t)Ntest * maxepoch);
@@ -1664,22 +1736,22 @@ extern "C" int gpt_cf_fullw_gibbs(
                             (int)n2, d_mp.as<int32_t>(), d_ml.as<int32_t>(), d_tu.as<int32_t>(),
                             d_tr.as<double>(), signal_var, su2, seed, sweep, kCfgV,
                             d_st.as<int32_t>(), nullptr);
-      if (e == hipSuccess)
+      if (e == hipSuccess && !fixw)
         e = launch_cfg_kron((int)r, d_U.as<double>(), (int)n1, d_V.as<double>(), (int)n2,
                             d_tu.as<int32_t>(), d_tm.as<int32_t>(), (int)N, d_A.as<double>(), nullptr);
-      if (e == hipSuccess)
+      if (e == hipSuccess && !fixw)
         e = gaussian_draw_dense(d_A.as<double>(), p, N, d_tr.as<double>(), 1.0 / signal_var,
                                 1.0 / (sigma_w * sigma_w), 1.0 / signal_var, seed, sweep, kCfgW, 0,
                                 d_M.as<double>(), d_x.as<double>(), d_z.as<double>(),
                                 d_w.as<double>(), d_st.as<int32_t>(), nullptr);
-      if (e != hipSuccess) return hip_fail(e, "GPT_fullw_gibbs sweep");
+      if (e != hipSuccess) return hip_fail(e, name);
     }
     int32_t bad = 0;
     HIPCHK(hipMemcpy(&bad, d_st.p, 4, hipMemcpyDeviceToHost));
     if (bad) { set_error("PosDefException: a Gibbs precision matrix is not positive definite"); return GPT_ERR_NOT_SPD; }
     if (epoch > burnin) {
       const int64_t s2 = epoch - burnin - 1;
-      HIPCHK(hipMemcpy(w_store + rr * s2, d_w.p, 8 * rr, hipMemcpyDeviceToHost));
+      if (w_store) HIPCHK(hipMemcpy(w_store + rr * s2, d_w.p, 8 * rr, hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(U_store + nU * s2, d_U.p, 8 * nU, hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(V_store + nV * s2, d_V.p, 8 * nV, hipMemcpyDeviceToHost));
       if (!avg) counter = 0;
@@ -1698,4 +1770,29 @@ extern "C" int gpt_cf_fullw_gibbs(
     }
   }
   return GPT_OK;
+}
+
+extern "C" int gpt_cf_fullw_gibbs(
+    const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2, const double* Ratingtest,
+    int64_t Ntest, int64_t ldt, double signal_var, double sigma_u, double sigma_w,
+    const double* w_init, int64_t r, int64_t burnin, int64_t maxepoch, int64_t n_samples,
+    uint64_t seed, double ytrainMean, double ytrainStd, int32_t avg, int32_t rotated_w,
+    double* w_store, double* U_store, double* V_store, double* testpred_store, double* trainRMSE,
+    double* testRMSE) {
+  return cf_gibbs_run("GPT_fullw_gibbs", Rating, N, ldr, n1, n2, Ratingtest, Ntest, ldt,
+                      signal_var, sigma_u, sigma_w, w_init, r, burnin, maxepoch, n_samples, seed,
+                      ytrainMean, ytrainStd, avg, rotated_w, false, w_store, U_store, V_store,
+                      testpred_store, trainRMSE, testRMSE);
+}
+
+extern "C" int gpt_cf_fixw_gibbs(
+    const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2, const double* Ratingtest,
+    int64_t Ntest, int64_t ldt, double signal_var, double sigma_u, const double* w, int64_t r,
+    int64_t burnin, int64_t maxepoch, int64_t n_samples, uint64_t seed, double ytrainMean,
+    double ytrainStd, int32_t avg, int32_t rotated_w, double* U_store, double* V_store,
+    double* testpred_store, double* trainRMSE, double* testRMSE) {
+  return cf_gibbs_run("GPT_fixw_gibbs", Rating, N, ldr, n1, n2, Ratingtest, Ntest, ldt,
+                      signal_var, sigma_u, 1.0, w, r, burnin, maxepoch, n_samples, seed,
+                      ytrainMean, ytrainStd, avg, rotated_w, true, nullptr, U_store, V_store,
+                      testpred_store, trainRMSE, testRMSE);
 }

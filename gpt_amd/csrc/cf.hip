@@ -243,7 +243,9 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     }
     __syncthreads();
     // gradw (:466, :473-477) and the w step of :479-483 into wn
+    // (GPT_fixw / GPT_fixw_sideinfo, :56-156 / :282-404: w is fixed — no gradw, no step)
     for (int o = tid; o < R * R; o += kCfNT) {
+      if (P.fixw) { wn_l[o] = w_l[o]; continue; }
       const int i = o % R, j = o / R;
       double g = 0.0;
       for (int ii = 0; ii < B; ++ii) g += er[ii] * (sU[ii * R + i] * sV[ii * R + j]) * is2;

@@ -189,6 +189,7 @@ struct CfParams {
   int n1, D1, n2, D2, r, m, rowsU, rowsV;
   double a, b, c, signal_var, sigma_u, sigma_w, epsw, epsU;
   int langevin, stiefel;
+  int fixw;              // GPT_fixw*: w is a fixed argument (no gradw, no w step)
   uint64_t seed;
   const int32_t* uptr;   // n1+1 CSR offsets into ufe: the feature rows (n1 + f) of each user
   const int32_t* ufe;

@@ -8,10 +8,21 @@ BASELINE config 5) on libgptsgld.so.
     GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w,
                     w_init, burnin, maxepoch, n_samples, param_seed, ytrainMean, ytrainStd;
                     avg=False, rotated_w=False)              100k_movielensExperiment.jl:1032-1129
+    GPT_fixw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, m, epsU,
+                      a, b, c, burnin, maxepoch, param_seed, ytrainMean, ytrainStd;
+                      langevin, stiefel, avg)                  :282-404
+    GPT_fullw(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w, w_init, m,
+              epsw, epsU, burnin, maxepoch, param_seed, ytrainMean, ytrainStd;
+              langevin, stiefel, avg)                          :160-279
+    GPT_fixw(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, m, epsU, burnin,
+             maxepoch, param_seed, ytrainMean, ytrainStd; langevin, stiefel, avg)     :56-156
+    GPT_fixw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, burnin,
+                   maxepoch, n_samples, param_seed, ytrainMean, ytrainStd; avg, rotated_w)
+                                                             :945-1028
     fold(data, i)     the standardised u{i}.base / u{i}.test split of :566-576
 
 Same argument meaning and return tuple as the reference: (w_store, U_store, V_store,
-testpred_store, trainRMSEvec, testRMSEvec).  ``data`` is the mapping written by
+testpred_store, trainRMSEvec, testRMSEvec), without w_store for the fixed-w variants.  ``data`` is the mapping written by
 scripts/make_ml100k_fixture.py (ratings per fold, the processed UserData / MovieData of
 :578-584).  Randomness follows the framework's Philox contract (oracle/movielens_ref.py).
 """
@@ -20,7 +31,8 @@ import numpy as np
 from ._lib import P_D, check, lib
 from . import _lib
 
-__all__ = ["GPT_fullw_sideinfo", "GPT_fullw_gibbs", "fold"]
+__all__ = ["GPT_fullw_sideinfo", "GPT_fixw_sideinfo", "GPT_fullw", "GPT_fixw", "GPT_fullw_gibbs",
+           "GPT_fixw_gibbs", "fold"]
 
 
 def _f64(a):
@@ -99,3 +111,97 @@ def GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u
         int(bool(rotated_w)), _ptr(w_store), _ptr(U_store), _ptr(V_store), _ptr(tps), _ptr(trm),
         _ptr(tsm)))
     return w_store, U_store, V_store, tps, trm, tsm
+
+
+def _sgd_common(Rating, Ratingtest, w, maxepoch):
+    Rt, Rs, w0 = _f64(Rating), _f64(Ratingtest), _f64(w)
+    r = w0.shape[0]
+    if Rt.shape[1] < 3 or Rs.shape[1] < 3 or w0.shape != (r, r):
+        raise ValueError("Rating / Ratingtest need (user, movie, rating) columns; w is r x r")
+    Ntest = Rs.shape[0]
+    return (Rt, Rs, w0, r, np.zeros((Ntest, maxepoch), order="F"), np.zeros(maxepoch),
+            np.zeros(maxepoch))
+
+
+def _nan_or_check(code):
+    if code == _lib.GPT_ERR_NAN_GEODESIC:
+        print("Get NaN when moving along Geodesic. Try smaller epsU")
+    else:
+        check(code)
+
+
+def GPT_fixw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, m, epsU,
+                      a, b, c, burnin, maxepoch, param_seed, ytrainMean, ytrainStd,
+                      langevin=False, stiefel=False, avg=False):
+    """100k_movielensExperiment.jl:282-404 -> (U_store, V_store, testpred_store, trainRMSEvec,
+    testRMSEvec)."""
+    Rt, Rs, w0, r, tps, trm, tsm = _sgd_common(Rating, Ratingtest, w, maxepoch)
+    Ud, Md = _f64(UserData), _f64(MovieData)
+    n1, D1 = Ud.shape
+    n2, D2 = Md.shape
+    U_store = np.zeros((n1 + D1, r, maxepoch), order="F")
+    V_store = np.zeros((n2 + D2, r, maxepoch), order="F")
+    _nan_or_check(lib().gpt_cf_fixw_sideinfo(
+        _ptr(Rt), Rt.shape[0], Rt.shape[0], _ptr(Ud), n1, D1, _ptr(Md), n2, D2, _ptr(Rs),
+        Rs.shape[0], Rs.shape[0], float(signal_var), float(sigma_u), _ptr(w0), r, int(m),
+        float(epsU), float(a), float(b), float(c), int(burnin), int(maxepoch),
+        int(param_seed) & (2 ** 64 - 1), float(ytrainMean), float(ytrainStd), int(bool(langevin)),
+        int(bool(stiefel)), int(bool(avg)), _ptr(U_store), _ptr(V_store), _ptr(tps), _ptr(trm),
+        _ptr(tsm)))
+    return U_store, V_store, tps, trm, tsm
+
+
+def GPT_fullw(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w, w_init, m,
+              epsw, epsU, burnin, maxepoch, param_seed, ytrainMean, ytrainStd, langevin=False,
+              stiefel=False, avg=False):
+    """100k_movielensExperiment.jl:160-279 (no side information) -> (w_store, U_store, V_store,
+    testpred_store, trainRMSEvec, testRMSEvec)."""
+    Rt, Rs, w0, r, tps, trm, tsm = _sgd_common(Rating, Ratingtest, w_init, maxepoch)
+    n1, n2 = np.shape(UserData)[0], np.shape(MovieData)[0]
+    w_store = np.zeros((r, r, maxepoch), order="F")
+    U_store = np.zeros((n1, r, maxepoch), order="F")
+    V_store = np.zeros((n2, r, maxepoch), order="F")
+    _nan_or_check(lib().gpt_cf_fullw(
+        _ptr(Rt), Rt.shape[0], Rt.shape[0], n1, n2, _ptr(Rs), Rs.shape[0], Rs.shape[0],
+        float(signal_var), float(sigma_u), float(sigma_w), _ptr(w0), r, int(m), float(epsw),
+        float(epsU), int(burnin), int(maxepoch), int(param_seed) & (2 ** 64 - 1),
+        float(ytrainMean), float(ytrainStd), int(bool(langevin)), int(bool(stiefel)),
+        int(bool(avg)), _ptr(w_store), _ptr(U_store), _ptr(V_store), _ptr(tps), _ptr(trm),
+        _ptr(tsm)))
+    return w_store, U_store, V_store, tps, trm, tsm
+
+
+def GPT_fixw(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, m, epsU, burnin,
+             maxepoch, param_seed, ytrainMean, ytrainStd, langevin=False, stiefel=False,
+             avg=False):
+    """100k_movielensExperiment.jl:56-156 (no side information, w fixed) -> (U_store, V_store,
+    testpred_store, trainRMSEvec, testRMSEvec)."""
+    Rt, Rs, w0, r, tps, trm, tsm = _sgd_common(Rating, Ratingtest, w, maxepoch)
+    n1, n2 = np.shape(UserData)[0], np.shape(MovieData)[0]
+    U_store = np.zeros((n1, r, maxepoch), order="F")
+    V_store = np.zeros((n2, r, maxepoch), order="F")
+    _nan_or_check(lib().gpt_cf_fixw(
+        _ptr(Rt), Rt.shape[0], Rt.shape[0], n1, n2, _ptr(Rs), Rs.shape[0], Rs.shape[0],
+        float(signal_var), float(sigma_u), _ptr(w0), r, int(m), float(epsU), int(burnin),
+        int(maxepoch), int(param_seed) & (2 ** 64 - 1), float(ytrainMean), float(ytrainStd),
+        int(bool(langevin)), int(bool(stiefel)), int(bool(avg)), _ptr(U_store), _ptr(V_store),
+        _ptr(tps), _ptr(trm), _ptr(tsm)))
+    return U_store, V_store, tps, trm, tsm
+
+
+def GPT_fixw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, burnin,
+                   maxepoch, n_samples, param_seed, ytrainMean, ytrainStd, avg=False,
+                   rotated_w=False):
+    """100k_movielensExperiment.jl:945-1028 -> (U_store, V_store, testpred_store, trainRMSEvec,
+    testRMSEvec)."""
+    Rt, Rs, w0, r, tps, trm, tsm = _sgd_common(Rating, Ratingtest, w, maxepoch)
+    n1, n2 = np.shape(UserData)[0], np.shape(MovieData)[0]
+    U_store = np.zeros((n1, r, maxepoch), order="F")
+    V_store = np.zeros((n2, r, maxepoch), order="F")
+    check(lib().gpt_cf_fixw_gibbs(
+        _ptr(Rt), Rt.shape[0], Rt.shape[0], n1, n2, _ptr(Rs), Rs.shape[0], Rs.shape[0],
+        float(signal_var), float(sigma_u), _ptr(w0), r, int(burnin), int(maxepoch),
+        int(n_samples), int(param_seed) & (2 ** 64 - 1), float(ytrainMean), float(ytrainStd),
+        int(bool(avg)), int(bool(rotated_w)), _ptr(U_store), _ptr(V_store), _ptr(tps), _ptr(trm),
+        _ptr(tsm)))
+    return U_store, V_store, tps, trm, tsm

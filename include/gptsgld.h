@@ -253,6 +253,55 @@ int gpt_cf_fullw_gibbs(const double* Rating, int64_t N, int64_t ldr, int64_t n1,
                        double* w_store, double* U_store, double* V_store, double* testpred_store,
                        double* trainRMSE, double* testRMSE);
 
+/* The other SGD / SGLD variants of the CF model (same Rating / Ratingtest / output conventions
+ * as gpt_cf_fullw_sideinfo; the NaN bail-out zeroes the parameter stores):
+ *   GPT_fixw_sideinfo(Rating,UserData,MovieData,Ratingtest,signal_var,sigma_u,w,m,epsU,a,b,c,
+ *     burnin,maxepoch,param_seed,ytrainMean,ytrainStd;langevin,stiefel,avg)
+ *     100k_movielensExperiment.jl:282-404 — w fixed, U,V = sigma_u*randn (also when stiefel);
+ *     returns U_store (n1+D1,r,T), V_store, testpred_store, trainRMSE, testRMSE.
+ *   GPT_fullw(Rating,UserData,MovieData,Ratingtest,signal_var,sigma_u,sigma_w,w_init,m,epsw,epsU,
+ *     burnin,maxepoch,param_seed,ytrainMean,ytrainStd;langevin,stiefel,avg)
+ *     :160-279 — no side information (pred = sum((U[user,:]*w).*V[movie,:])), U,V = randn or
+ *     the Stiefel polar init; returns w_store (r,r,T), U_store (n1,r,T), V_store (n2,r,T), ...
+ *   GPT_fixw(Rating,UserData,MovieData,Ratingtest,signal_var,sigma_u,w,m,epsU,burnin,maxepoch,
+ *     param_seed,ytrainMean,ytrainStd;langevin,stiefel,avg)
+ *     :56-156 — no side information, w fixed, U,V = sigma_u*randn; returns U_store (n1,r,T), ...
+ * (The reference's bail-out of GPT_fullw / GPT_fixw returns a 3-tuple of zero arrays; these
+ * entry points keep the normal outputs with zeroed parameter stores and GPT_ERR_NAN_GEODESIC.) */
+int gpt_cf_fixw_sideinfo(const double* Rating, int64_t N, int64_t ldr, const double* UserData,
+                         int64_t n1, int64_t D1, const double* MovieData, int64_t n2, int64_t D2,
+                         const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var,
+                         double sigma_u, const double* w, int64_t r, int64_t m, double epsU,
+                         double a, double b, double c, int64_t burnin, int64_t maxepoch,
+                         uint64_t seed, double ytrainMean, double ytrainStd, int32_t langevin,
+                         int32_t stiefel, int32_t avg, double* U_store, double* V_store,
+                         double* testpred_store, double* trainRMSE, double* testRMSE);
+int gpt_cf_fullw(const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2,
+                 const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var,
+                 double sigma_u, double sigma_w, const double* w_init, int64_t r, int64_t m,
+                 double epsw, double epsU, int64_t burnin, int64_t maxepoch, uint64_t seed,
+                 double ytrainMean, double ytrainStd, int32_t langevin, int32_t stiefel,
+                 int32_t avg, double* w_store, double* U_store, double* V_store,
+                 double* testpred_store, double* trainRMSE, double* testRMSE);
+int gpt_cf_fixw(const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2,
+                const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var,
+                double sigma_u, const double* w, int64_t r, int64_t m, double epsU, int64_t burnin,
+                int64_t maxepoch, uint64_t seed, double ytrainMean, double ytrainStd,
+                int32_t langevin, int32_t stiefel, int32_t avg, double* U_store, double* V_store,
+                double* testpred_store, double* trainRMSE, double* testRMSE);
+
+/* GPT_fixw_gibbs(Rating,UserData,MovieData,Ratingtest,signal_var,sigma_u,w,burnin,maxepoch,
+ *   n_samples,param_seed;avg,rotated_w)  100k_movielensExperiment.jl:945-1028: the user / movie
+ * Gibbs conditionals of gpt_cf_fullw_gibbs with w fixed (no w draw); returns U_store (n1,r,T),
+ * V_store (n2,r,T), testpred_store, trainRMSE, testRMSE. */
+int gpt_cf_fixw_gibbs(const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2,
+                      const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var,
+                      double sigma_u, const double* w, int64_t r, int64_t burnin,
+                      int64_t maxepoch, int64_t n_samples, uint64_t seed, double ytrainMean,
+                      double ytrainStd, int32_t avg, int32_t rotated_w, double* U_store,
+                      double* V_store, double* testpred_store, double* trainRMSE,
+                      double* testRMSE);
+
 /* randperm(N) + phi = phi[:,:,perm] of GPT_SGLD.jl:373-374 for `epochs` epochs of one chain,
  * built on the device by the sessions' own kernel: out (N, epochs) column-major, 0-based rows
  * of the composed order (order_e = order_{e-1}[perm_e]). */

@@ -39,11 +39,15 @@ def uv_noise(rows, r, seed, step, which):
     return px.normals(re * rows, seed, step, px.CF_UV_NOISE, which).reshape((rows, re))[:, :r]
 
 
-def init_uv(rows, r, seed, which, stiefel, sigma_u):
-    if stiefel:
+def init_uv(rows, r, seed, which, stiefel, sigma_u, mode="side"):
+    """U / V init: "side" (GPT_fullw_sideinfo :424-428) Stiefel polar factor or σ_u·randn;
+    "sigma" (GPT_fixw*, :67 / :294) σ_u·randn also when stiefel; "unit" (GPT_fullw :175-180)
+    polar factor or randn."""
+    if stiefel and mode != "sigma":
         z = px.normals(r * rows, seed, 0, px.CF_UV_INIT, which).reshape((r, rows), order="F")
         return np.asfortranarray(R.stiefel_init(z))
-    return sigma_u * px.normals(rows * r, seed, 0, px.CF_UV_INIT, which).reshape((rows, r), order="F")
+    z = px.normals(rows * r, seed, 0, px.CF_UV_INIT, which).reshape((rows, r), order="F")
+    return z if mode == "unit" else sigma_u * z
 
 
 def predict(ratings, U, V, w, uidx, vidx, a, b, c):
@@ -58,8 +62,9 @@ def predict(ratings, U, V, w, uidx, vidx, a, b, c):
 
 def GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w,
                        w_init, m, epsw, epsU, a, b, c, burnin, maxepoch, param_seed, ytrainMean,
-                       ytrainStd, langevin=False, stiefel=False, avg=False):
-    """100k_movielensExperiment.jl:409-551.  Rating (N, 3+) holds 1-based user / movie ids and
+                       ytrainStd, langevin=False, stiefel=False, avg=False, fixw=False,
+                       init="side"):
+    """100k_movielensExperiment.jl:409-551 (fixw / init: the other SGD variants, below).  Rating (N, 3+) holds 1-based user / movie ids and
     the standardised rating.  Returns (w_store (r, r, T), U_store (n1+D1, r, T), V_store,
     testpred_store (Ntest, T), trainRMSEvec (T), testRMSEvec (T)), T = maxepoch; entries of
     epochs after an early stop (:545-547) stay 0 (10 for testRMSEvec, as :441)."""
@@ -75,8 +80,8 @@ def GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigm
     U_store = np.zeros((n1 + D1, r, maxepoch), order="F")
     V_store = np.zeros((n2 + D2, r, maxepoch), order="F")
     testpred_store = np.zeros((Ntest, maxepoch), order="F")
-    U = init_uv(n1 + D1, r, param_seed, 0, stiefel, sigma_u)
-    V = init_uv(n2 + D2, r, param_seed, 1, stiefel, sigma_u)
+    U = init_uv(n1 + D1, r, param_seed, 0, stiefel, sigma_u, init)
+    V = init_uv(n2 + D2, r, param_seed, 1, stiefel, sigma_u, init)
     uidx, vidx = side_rows(UserData, MovieData)
     trainRMSE = np.zeros(maxepoch)
     testRMSE = 10.0 * np.ones(maxepoch)
@@ -113,9 +118,10 @@ def GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigm
             gradw = gradw * N / B - w / sigma_w ** 2
             gradU *= N / B
             gradV *= N / B
-            w = w + epsw * gradw / 2
-            if langevin:
-                w = w + sqw * px.normals(r * r, param_seed, step, px.CF_W_NOISE, 0).reshape((r, r), order="F")
+            if not fixw:                                             # GPT_fixw*: w is fixed
+                w = w + epsw * gradw / 2
+                if langevin:
+                    w = w + sqw * px.normals(r * r, param_seed, step, px.CF_W_NOISE, 0).reshape((r, r), order="F")
             new = []
             for which, (M, G) in enumerate(((U, gradU), (V, gradV))):
                 xi = uv_noise(M.shape[0], r, param_seed, step, which)
@@ -155,9 +161,60 @@ def GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigm
     return w_store, U_store, V_store, testpred_store, trainRMSE, testRMSE
 
 
+def GPT_fixw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, m, epsU,
+                      a, b, c, burnin, maxepoch, param_seed, ytrainMean, ytrainStd,
+                      langevin=False, stiefel=False, avg=False):
+    """100k_movielensExperiment.jl:282-404: GPT_fullw_sideinfo with w fixed (no gradw, no w
+    step) and U, V = σ_u·randn (:294, also under stiefel).  Returns (U_store, V_store,
+    testpred_store, trainRMSE, testRMSE)."""
+    out = GPT_fullw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, 1.0, w,
+                             m, 0.0, epsU, a, b, c, burnin, maxepoch, param_seed, ytrainMean,
+                             ytrainStd, langevin, stiefel, avg, fixw=True, init="sigma")
+    return out[1:]
+
+
+def _no_side(UserData, MovieData):
+    return np.zeros((np.shape(UserData)[0], 0)), np.zeros((np.shape(MovieData)[0], 0))
+
+
+def GPT_fullw(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w, w_init, m,
+              epsw, epsU, burnin, maxepoch, param_seed, ytrainMean, ytrainStd, langevin=False,
+              stiefel=False, avg=False):
+    """100k_movielensExperiment.jl:160-279: no side information — pred = sum((U[user,:]*w).*
+    V[movie,:]), gradw = kron(V[movie,:]', U[user,:]') (= the side-information model at a = 1,
+    b = c = 0 with no feature rows); U, V = randn or the Stiefel polar init (:175-180)."""
+    ud, md = _no_side(UserData, MovieData)
+    return GPT_fullw_sideinfo(Rating, ud, md, Ratingtest, signal_var, sigma_u, sigma_w, w_init, m,
+                              epsw, epsU, 1.0, 0.0, 0.0, burnin, maxepoch, param_seed, ytrainMean,
+                              ytrainStd, langevin, stiefel, avg, init="unit")
+
+
+def GPT_fixw(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, m, epsU, burnin,
+             maxepoch, param_seed, ytrainMean, ytrainStd, langevin=False, stiefel=False,
+             avg=False):
+    """100k_movielensExperiment.jl:56-156: no side information, w fixed, U, V = σ_u·randn.
+    Returns (U_store, V_store, testpred_store, trainRMSE, testRMSE)."""
+    ud, md = _no_side(UserData, MovieData)
+    out = GPT_fullw_sideinfo(Rating, ud, md, Ratingtest, signal_var, sigma_u, 1.0, w, m, 0.0,
+                             epsU, 1.0, 0.0, 0.0, burnin, maxepoch, param_seed, ytrainMean,
+                             ytrainStd, langevin, stiefel, avg, fixw=True, init="sigma")
+    return out[1:]
+
+
+def GPT_fixw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, burnin,
+                   maxepoch, n_samples, param_seed, ytrainMean, ytrainStd, avg=False,
+                   rotated_w=False):
+    """100k_movielensExperiment.jl:945-1028: the user / movie conditionals of GPT_fullw_gibbs
+    with w fixed (no w draw).  Returns (U_store, V_store, testpred_store, trainRMSE, testRMSE)."""
+    out = GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, 1.0, w,
+                          burnin, maxepoch, n_samples, param_seed, ytrainMean, ytrainStd, avg,
+                          rotated_w, fixw=True)
+    return out[1:]
+
+
 def GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w, w_init,
                     burnin, maxepoch, n_samples, param_seed, ytrainMean, ytrainStd, avg=False,
-                    rotated_w=False):
+                    rotated_w=False, fixw=False):
     r"""100k_movielensExperiment.jl:1032-1129 — Gibbs sampling of the tensor CF model without
     side information: per sweep every user row U_i | V, w, every movie row V_j | U, w (r × r
     Gaussian conditionals through chol(·,:U)), then w | U, V with the N × r² Kronecker design
@@ -215,10 +272,11 @@ def GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u
                     X = U[users[sel]] @ w
                     prec = X.T @ X / signal_var + np.eye(r) / sigma_u ** 2
                     V[j] = draw(prec, X.T @ y[sel], px.normals(r, param_seed, sweep, px.CFG_V, j))
-            K = (V[movies][:, :, None] * U[users][:, None, :]).reshape((N, r * r))   # kron(V, U)
-            prec = K.T @ K / signal_var + np.eye(r * r) / sigma_w ** 2                  # :1092
-            w = draw(prec, K.T @ y, px.normals(r * r, param_seed, sweep, px.CFG_W, 0)).reshape(
-                (r, r), order="F")
+            if not fixw:
+                K = (V[movies][:, :, None] * U[users][:, None, :]).reshape((N, r * r))   # kron(V, U)
+                prec = K.T @ K / signal_var + np.eye(r * r) / sigma_w ** 2              # :1092
+                w = draw(prec, K.T @ y, px.normals(r * r, param_seed, sweep, px.CFG_W, 0)).reshape(
+                    (r, r), order="F")
             sweep += 1
         if epoch > burnin:
             s = epoch - burnin - 1

@@ -94,3 +94,81 @@ def test_fullw_gibbs_matches_oracle(name):
     assert np.abs(got[3] - want[3]).max() < 1e-8
     assert np.all(np.abs(got[4] - want[4]) <= 1e-9 * want[4])
     assert np.all(np.abs(got[5] - want[5]) <= 1e-9 * want[5])
+
+
+# The other CF variants of 100k_movielensExperiment.jl: GPT_fixw_sideinfo (:282-404), GPT_fullw
+# (:160-279), GPT_fixw (:56-156) on the same device kernels (w fixed / no feature rows / their
+# own U, V initialisations), GPT_fixw_gibbs (:945-1028) on the Gibbs kernels without the w draw.
+VARIANT_CASES = {
+    # name: (ntrain, ntest, r, m, epochs, burnin, langevin, stiefel, avg, epsU)
+    "sgd_euclid": (3000, 1000, 4, 100, 2, 0, False, False, False, 1e-6),
+    "sgld_euclid_avg": (2950, 800, 5, 64, 3, 1, True, False, True, 1e-6),
+    "sgld_stiefel": (2950, 800, 3, 64, 2, 0, True, True, True, 1e-4),
+}
+
+
+def _check_tail(got, want):
+    """(…, testpred_store, trainRMSE, testRMSE) tails of the variant tuples."""
+    assert np.abs(got[-3] - want[-3]).max() < 1e-8
+    assert np.all(np.abs(got[-2] - want[-2]) <= 1e-9 * want[-2])
+    assert np.all(np.abs(got[-1] - want[-1]) <= 1e-9 * want[-1])
+
+
+@pytest.mark.parametrize("name", list(VARIANT_CASES))
+def test_fixw_sideinfo_matches_oracle(name):
+    from gpt_amd import movielens
+    ntr, nte, r, m, ep, bi, lang, stf, avg, epsU = VARIANT_CASES[name]
+    tr, te, ud, md, mu, sd = problem(ntr, nte)
+    w = np.random.default_rng(6).standard_normal((r, r))
+    args = (tr, ud, md, te, 0.8, 0.1, w, m, epsU, 0.5, 0.25, 0.5, bi, ep, 17, mu, sd)
+    got = movielens.GPT_fixw_sideinfo(*args, langevin=lang, stiefel=stf, avg=avg)
+    want = M.GPT_fixw_sideinfo(*args, langevin=lang, stiefel=stf, avg=avg)
+    assert len(got) == len(want) == 5
+    assert got[0].shape == (ud.shape[0] + ud.shape[1], r, ep)
+    for g, w_ in zip(got[:2], want[:2]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    _check_tail(got, want)
+
+
+@pytest.mark.parametrize("name", list(VARIANT_CASES))
+def test_fullw_no_side_matches_oracle(name):
+    from gpt_amd import movielens
+    ntr, nte, r, m, ep, bi, lang, stf, avg, epsU = VARIANT_CASES[name]
+    tr, te, ud, md, mu, sd = problem(ntr, nte)
+    w0 = np.random.default_rng(7).standard_normal((r, r))
+    args = (tr, ud, md, te, 0.8, 0.1, 1.0, w0, m, 1e-4, epsU, bi, ep, 17, mu, sd)
+    got = movielens.GPT_fullw(*args, langevin=lang, stiefel=stf, avg=avg)
+    want = M.GPT_fullw(*args, langevin=lang, stiefel=stf, avg=avg)
+    assert got[1].shape == (ud.shape[0], r, ep)                   # no feature rows
+    for g, w_ in zip(got[:3], want[:3]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    _check_tail(got, want)
+
+
+@pytest.mark.parametrize("name", list(VARIANT_CASES))
+def test_fixw_no_side_matches_oracle(name):
+    from gpt_amd import movielens
+    ntr, nte, r, m, ep, bi, lang, stf, avg, epsU = VARIANT_CASES[name]
+    tr, te, ud, md, mu, sd = problem(ntr, nte)
+    w = np.random.default_rng(8).standard_normal((r, r))
+    args = (tr, ud, md, te, 0.8, 0.1, w, m, epsU, bi, ep, 17, mu, sd)
+    got = movielens.GPT_fixw(*args, langevin=lang, stiefel=stf, avg=avg)
+    want = M.GPT_fixw(*args, langevin=lang, stiefel=stf, avg=avg)
+    assert len(got) == 5 and got[0].shape == (ud.shape[0], r, ep)
+    for g, w_ in zip(got[:2], want[:2]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    _check_tail(got, want)
+
+
+@pytest.mark.parametrize("rotated", [False, True])
+def test_fixw_gibbs_matches_oracle(rotated):
+    from gpt_amd import movielens
+    tr, te, ud, md, mu, sd = problem(3000, 800)
+    w = np.random.default_rng(9).standard_normal((4, 4))
+    args = (tr, ud, md, te, 0.8, 0.5, w, 1, 2, 2, 17, mu, sd)
+    got = movielens.GPT_fixw_gibbs(*args, avg=True, rotated_w=rotated)
+    want = M.GPT_fixw_gibbs(*args, avg=True, rotated_w=rotated)
+    assert len(got) == 5
+    for g, w_ in zip(got[:2], want[:2]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    _check_tail(got, want)
