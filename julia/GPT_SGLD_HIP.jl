@@ -55,6 +55,17 @@ function feature(X::Array{Float64,2}, n::Integer, length_scale, sigma_RBF::Real,
     return feature(X, length_scale, sigma_RBF, scale, Z, b)
 end
 
+# Generation-A seeded form feature(X,n,length_scale,seed) (GPT_SGLD_p.jl:40-54): Z = randn(n,D)
+# / length_scale, b = randn(n,D), phi = sqrt(2/n)·cos(X[i,k]·Z[j,k] + b[j,k]) — no sigma_RBF, no
+# scale (gpt_feature_inputs_a draws Z and b on the framework's Philox contract)
+function feature(X::Array{Float64,2}, n::Integer, length_scale::Real, seed::Integer)
+    D = size(X, 2)
+    Z = Array{Float64}(undef, n, D); b = Array{Float64}(undef, n, D)
+    check(ccall((:gpt_feature_inputs_a, LIB), Cint, (Int64, Int64, UInt64, Ptr{Float64}, Ptr{Float64}),
+                n, D, seed, Z, b))
+    return feature(X, 1.0, 1.0, 1.0, Z ./ length_scale, b)
+end
+
 # featureNotensor(X,length_scale,sigma_RBF,Z,b)  GPT_SGLD.jl:109
 function featureNotensor(X::Array{Float64,2}, length_scale, sigma_RBF::Real, Z::Array{Float64,2},
                          b::Array{Float64})
