@@ -264,6 +264,7 @@ def main():
                        engine=args.engine)
     info = sess.info()
     warm_ms = 0.0
+    warm_steps = 0                     # chain steps of the scratch session (profile accounting)
     if args.clock_warm_ms > 0:
         # bring the GPU to its sustained clock before the timed region (a fresh box idles at low
         # clocks; the driver's --warmup 5 is ~1 ms of work): a scratch session of the same shape
@@ -277,8 +278,10 @@ def main():
                 sw = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var,
                                  0, 2, [10 ** 6 + c for c in range(C)], store=False,
                                  engine=args.engine)
-            sw.run(min(nb, sw.total_steps - sw.steps_done))
+            ns = min(nb, sw.total_steps - sw.steps_done)
+            sw.run(ns)
             sw.sync()
+            warm_steps += ns
         warm_ms = (time.perf_counter() - tw) * 1000.0
         sw.close()
     sess.run(args.warmup)
@@ -433,7 +436,7 @@ def main():
                                            "launch, total / steps)",
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "algorithmic_bytes_per_step": bytes_launch,
-                         "steps_run_per_chain": sess.total_steps},
+                         "steps_run_per_chain": sess.total_steps + warm_steps},
             "cpu_baseline": cpu,
             "test_rmse": quality["test_rmse"],
             "test_rmse_note": quality["note"],
