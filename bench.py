@@ -304,7 +304,7 @@ def main():
     # per-launch kernel time (hipEvents around each step-kernel launch on the session stream)
     k_us = sess.time_steps(args.kernel_steps)
     sess.sync()
-    bad = [c for c in range(C) if sess.fetch(c)[2] != 0]
+    bad = [c for c in range(C) if sess.status(c) != 0]
     if bad:
         raise SystemExit("chains %s hit the geodesic NaN bail-out: the timed steps were no-ops" % bad)
     B = m
@@ -335,7 +335,7 @@ def main():
     sess.run(sess.total_steps)
     sess.sync()
     quality_train_s = time.perf_counter() - tq
-    status = [sess.fetch(c)[2] for c in range(C)]
+    status = [sess.status(c) for c in range(C)]
     fsum_q = torch.zeros(Nte, dtype=torch.float64, device=dev)
     cnt = 0
     fhq = torch.empty((last, Nte), dtype=torch.float64, device=dev)

@@ -98,6 +98,15 @@ SIGNATURES = {
                                      C.c_int64, C.c_int64, C.c_int64, C.c_uint64, C.c_double,
                                      C.c_double, C.c_int32, C.c_int32, P_D, P_D, P_D, P_D, P_D,
                                      P_D]),
+    "gpt_cf_fullw_sideinfo_folds": (C.c_int, [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, P_D, C.c_int64, C.c_int64, P_D,
+                                              C.c_int64, C.c_int64, C.c_double, C.c_double,
+                                              C.c_double, P_D, C.c_int64, C.c_int64, C.c_double,
+                                              C.c_double, C.c_double, C.c_double, C.c_double,
+                                              C.c_int64, C.c_int64, C.c_uint64, P_D, P_D,
+                                              C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, P_I32]),
     "gpt_cf_fixw_sideinfo": (C.c_int, [P_D, C.c_int64, C.c_int64, P_D, C.c_int64, C.c_int64, P_D,
                                        C.c_int64, C.c_int64, P_D, C.c_int64, C.c_int64,
                                        C.c_double, C.c_double, P_D, C.c_int64, C.c_int64,

@@ -1378,44 +1378,49 @@ static void cf_features(const double* X, int n, int D, int rowbase, std::vector<
 //   kCfInitUnit  GPT_fullw :175-180           stiefel ? polar(randn(r,rows)) : randn(rows,r)
 enum CfInit { kCfInitSide = 0, kCfInitSigma = 1, kCfInitUnit = 2 };
 
-// One SGD / SGLD run of the tensor CF model (the body of every GPT_*w* SGD variant): fixw keeps
-// w at w_init (w_store may then be null), D1 = D2 = 0 with a = 1, b = c = 0 is the model without
-// side information.
+// One fold's ratings and outputs of a CF run (column-major, caller-owned).
+struct CfFold {
+  const double* Rating; int64_t N, ldr;
+  const double* Ratingtest; int64_t Ntest, ldt;
+  double ymean, ystd;
+  double *w_store, *U_store, *V_store, *testpred_store, *trainRMSE, *testRMSE;
+  int32_t status;                  // out: GPT_OK or GPT_ERR_NAN_GEODESIC
+};
+
+// SGD / SGLD runs of the tensor CF model (the body of every GPT_*w* SGD variant) for F folds at
+// once: the folds are sibling chains of one cf_epoch_kernel launch per epoch (the reference runs
+// them as `@parallel for i=1:5`, 100k_movielensExperiment.jl:733-736), each with its own ratings,
+// permutation, state, evaluation and early stop (:541-547); a fold that stops or bails out is
+// skipped by later launches.  The folds share the side information, hyper-parameters and seed,
+// hence the initial U, V (as separate calls with one param_seed do) and the per-epoch
+// permutation; every fold has the same number of training ratings.  fixw keeps w at w_init
+// (w_store may then be null); D1 = D2 = 0 with a = 1, b = c = 0 is the model without side
+// information.
 static int cf_sgd_run(
-    const char* name, const double* Rating, int64_t N, int64_t ldr, const double* UserData,
-    int64_t n1, int64_t D1, const double* MovieData, int64_t n2, int64_t D2,
-    const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var, double sigma_u,
+    const char* name, std::vector<CfFold>& folds, const double* UserData, int64_t n1, int64_t D1,
+    const double* MovieData, int64_t n2, int64_t D2, double signal_var, double sigma_u,
     double sigma_w, const double* w_init, int64_t r, int64_t m, double epsw, double epsU, double a,
-    double b, double c, int64_t burnin, int64_t maxepoch, uint64_t seed, double ytrainMean,
-    double ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg, bool fixw, CfInit init,
-    double* w_store, double* U_store, double* V_store, double* testpred_store, double* trainRMSE,
-    double* testRMSE) {
-  if (!Rating || (D1 > 0 && !UserData) || (D2 > 0 && !MovieData) || !Ratingtest || !w_init ||
-      (!fixw && !w_store) || !U_store ||
-      !V_store || !testpred_store || !trainRMSE || !testRMSE || N < 1 || Ntest < 1 || ldr < N ||
-      ldt < Ntest || n1 < 1 || n2 < 1 || D1 < 0 || D2 < 0 || m < 1 || burnin < 0 || maxepoch < 0 ||
-      !(signal_var > 0) || !(sigma_u > 0) || !(sigma_w > 0)) {
-    set_error(std::string("bad ") + name + " arguments"); return GPT_ERR_BAD_DIMS;
-  }
+    double b, double c, int64_t burnin, int64_t maxepoch, uint64_t seed, int32_t langevin,
+    int32_t stiefel, int32_t avg, bool fixw, CfInit init) {
+  const int F = (int)folds.size();
+  bool ok = F >= 1 && (D1 == 0 || UserData) && (D2 == 0 || MovieData) && w_init && n1 >= 1 &&
+            n2 >= 1 && D1 >= 0 && D2 >= 0 && m >= 1 && burnin >= 0 && maxepoch >= 0 &&
+            signal_var > 0 && sigma_u > 0 && sigma_w > 0;
+  for (const CfFold& f : folds)
+    ok = ok && f.Rating && f.Ratingtest && (fixw || f.w_store) && f.U_store && f.V_store &&
+         f.testpred_store && f.trainRMSE && f.testRMSE && f.N >= 1 && f.Ntest >= 1 &&
+         f.ldr >= f.N && f.ldt >= f.Ntest && f.N == folds[0].N;
+  if (!ok) { set_error(std::string("bad ") + name + " arguments"); return GPT_ERR_BAD_DIMS; }
   if (!cf_rank_supported((int)r) || cf_lds_bytes((int)r, (int)m) > 160 * 1024) {
     set_error(std::string(name) + ": rank not instantiated (1-6,8,10,12,15,16,20) or minibatch too large");
     return GPT_ERR_BAD_DIMS;
   }
+  const int64_t N = folds[0].N;
   const int rowsU = (int)(n1 + D1), rowsV = (int)(n2 + D2);
-  std::vector<int32_t> tu(N), tm(N), eu(Ntest), em(Ntest);
-  std::vector<double> tr(N), er(Ntest);
-  for (int64_t i = 0; i < N; ++i) {
-    tu[i] = (int32_t)Rating[i] - 1; tm[i] = (int32_t)Rating[i + ldr] - 1; tr[i] = Rating[i + 2 * ldr];
-    if (tu[i] < 0 || tu[i] >= n1 || tm[i] < 0 || tm[i] >= n2) { set_error("rating ids out of range"); return GPT_ERR_BAD_DIMS; }
-  }
-  for (int64_t i = 0; i < Ntest; ++i) {
-    eu[i] = (int32_t)Ratingtest[i] - 1; em[i] = (int32_t)Ratingtest[i + ldt] - 1; er[i] = Ratingtest[i + 2 * ldt];
-    if (eu[i] < 0 || eu[i] >= n1 || em[i] < 0 || em[i] >= n2) { set_error("test rating ids out of range"); return GPT_ERR_BAD_DIMS; }
-  }
   std::vector<int32_t> uptr, ufe, vptr, vfe;
   cf_features(UserData, (int)n1, (int)D1, (int)n1, uptr, ufe);
   cf_features(MovieData, (int)n2, (int)D2, (int)n2, vptr, vfe);
-  // U, V init (:424-428): Stiefel polar factor of Z = randn(r, rows) or sigma_u·randn(rows, r)
+  // U, V init (:424-428 / :67 / :175-180, see CfInit)
   std::vector<double> U0((size_t)rowsU * r), V0((size_t)rowsV * r);
   for (int which = 0; which < 2; ++which) {
     const int rows = which ? rowsV : rowsU;
@@ -1428,33 +1433,70 @@ static int cf_sgd_run(
   }
   const size_t nU = U0.size(), nV = V0.size(), rr = (size_t)r * r;
   const int nbatch = (int)((N + m - 1) / m);
-  const int neval = (int)((std::max(N, Ntest) + 255) / 256);
-  DevMem d_tu, d_tm, d_tr, d_eu, d_em, d_er, d_up, d_uf, d_vp, d_vf, d_perm, d_w, d_U, d_V, d_GU,
-      d_GV, d_trp, d_tep, d_sse, d_st, d_ch;
-  HIPCHK(d_tu.alloc(4 * N)); HIPCHK(d_tm.alloc(4 * N)); HIPCHK(d_tr.alloc(8 * N));
-  HIPCHK(d_eu.alloc(4 * Ntest)); HIPCHK(d_em.alloc(4 * Ntest)); HIPCHK(d_er.alloc(8 * Ntest));
+  int64_t ntmax = 0;
+  for (const CfFold& f : folds) ntmax = std::max(ntmax, f.Ntest);
+  const int nmax = (int)std::max(N, ntmax);
+  const int neval = (nmax + 255) / 256;
+  DevMem d_up, d_uf, d_vp, d_vf, d_perm, d_ch;
   HIPCHK(d_up.alloc(4 * uptr.size())); HIPCHK(d_uf.alloc(4 * ufe.size()));
   HIPCHK(d_vp.alloc(4 * vptr.size())); HIPCHK(d_vf.alloc(4 * vfe.size()));
-  HIPCHK(d_perm.alloc(4 * N)); HIPCHK(d_w.alloc(8 * rr)); HIPCHK(d_U.alloc(8 * nU));
-  HIPCHK(d_V.alloc(8 * nV)); HIPCHK(d_GU.alloc(8 * nU)); HIPCHK(d_GV.alloc(8 * nV));
-  HIPCHK(d_trp.alloc(8 * N)); HIPCHK(d_tep.alloc(8 * Ntest)); HIPCHK(d_sse.alloc(16 * (size_t)neval));
-  HIPCHK(d_st.alloc(4)); HIPCHK(d_ch.alloc(sizeof(CfChain)));
-  HIPCHK(hipMemcpy(d_tu.p, tu.data(), 4 * N, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_tm.p, tm.data(), 4 * N, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_tr.p, tr.data(), 8 * N, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_eu.p, eu.data(), 4 * Ntest, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_em.p, em.data(), 4 * Ntest, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_er.p, er.data(), 8 * Ntest, hipMemcpyHostToDevice));
+  HIPCHK(d_perm.alloc(4 * N)); HIPCHK(d_ch.alloc(sizeof(CfChain) * F));
   HIPCHK(hipMemcpy(d_up.p, uptr.data(), 4 * uptr.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_uf.p, ufe.data(), 4 * ufe.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_vp.p, vptr.data(), 4 * vptr.size(), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_vf.p, vfe.data(), 4 * vfe.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_w.p, w_init, 8 * rr, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_U.p, U0.data(), 8 * nU, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_V.p, V0.data(), 8 * nV, hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(d_GU.p, 0, 8 * nU)); HIPCHK(hipMemset(d_GV.p, 0, 8 * nV));
-  HIPCHK(hipMemset(d_trp.p, 0, 8 * N)); HIPCHK(hipMemset(d_tep.p, 0, 8 * Ntest));
-  HIPCHK(hipMemset(d_st.p, 0, 4));
+  // per fold: ratings, state, scratch, running predictions, SSE partials, status
+  std::vector<std::unique_ptr<DevMem>> mem;
+  std::vector<CfChain> ch(F);
+  std::vector<int32_t*> d_st(F);
+  std::vector<double*> d_w(F), d_U(F), d_V(F), d_sse(F), d_tep(F);
+  for (int f = 0; f < F; ++f) {
+    const CfFold& fd = folds[f];
+    const int64_t Nt = fd.Ntest;
+    std::vector<int32_t> tu(N), tm(N), eu(Nt), em(Nt);
+    std::vector<double> tr(N), er(Nt);
+    for (int64_t i = 0; i < N; ++i) {
+      tu[i] = (int32_t)fd.Rating[i] - 1; tm[i] = (int32_t)fd.Rating[i + fd.ldr] - 1;
+      tr[i] = fd.Rating[i + 2 * fd.ldr];
+      if (tu[i] < 0 || tu[i] >= n1 || tm[i] < 0 || tm[i] >= n2) { set_error("rating ids out of range"); return GPT_ERR_BAD_DIMS; }
+    }
+    for (int64_t i = 0; i < Nt; ++i) {
+      eu[i] = (int32_t)fd.Ratingtest[i] - 1; em[i] = (int32_t)fd.Ratingtest[i + fd.ldt] - 1;
+      er[i] = fd.Ratingtest[i + 2 * fd.ldt];
+      if (eu[i] < 0 || eu[i] >= n1 || em[i] < 0 || em[i] >= n2) { set_error("test rating ids out of range"); return GPT_ERR_BAD_DIMS; }
+    }
+    // one allocation per fold: ids (int32) first, then doubles (8-B aligned offsets)
+    const size_t ints = (size_t)(2 * N + 2 * Nt + 2);
+    const size_t dbl0 = (ints * 4 + 15) / 16 * 2;                     // in doubles
+    const size_t ndbl = (size_t)N + Nt + rr + 2 * nU + 2 * nV + N + Nt + 2 * (size_t)neval;
+    std::unique_ptr<DevMem> dm(new DevMem());
+    HIPCHK(dm->alloc(8 * (dbl0 + ndbl)));
+    int32_t* ip = dm->as<int32_t>();
+    double* dp = dm->as<double>() + dbl0;
+    CfChain& C = ch[f];
+    C.tr_user = ip; C.tr_movie = ip + N; C.te_user = ip + 2 * N; C.te_movie = ip + 2 * N + Nt;
+    d_st[f] = ip + 2 * N + 2 * Nt;
+    C.tr_rating = dp; C.te_rating = dp + N;
+    C.w = dp + N + Nt; C.U = C.w + rr; C.V = C.U + nU; C.GU = C.V + nV; C.GV = C.GU + nU;
+    C.trainpred = C.GV + nV; C.testpred = C.trainpred + N; C.sse = C.testpred + Nt;
+    C.N = (int)N; C.Ntest = (int)Nt; C.perm = d_perm.as<int32_t>();
+    C.status = d_st[f]; C.ymean = fd.ymean; C.ystd = fd.ystd;
+    d_w[f] = C.w; d_U[f] = C.U; d_V[f] = C.V; d_sse[f] = C.sse; d_tep[f] = C.testpred;
+    HIPCHK(hipMemcpy((void*)C.tr_user, tu.data(), 4 * N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void*)C.tr_movie, tm.data(), 4 * N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void*)C.te_user, eu.data(), 4 * Nt, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void*)C.te_movie, em.data(), 4 * Nt, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void*)C.tr_rating, tr.data(), 8 * N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy((void*)C.te_rating, er.data(), 8 * Nt, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(C.w, w_init, 8 * rr, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(C.U, U0.data(), 8 * nU, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(C.V, V0.data(), 8 * nV, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(C.GU, 0, 8 * (nU + nV)));                             // GU, GV
+    HIPCHK(hipMemset(C.trainpred, 0, 8 * (size_t)(N + Nt)));
+    HIPCHK(hipMemset(d_st[f], 0, 4));
+    mem.push_back(std::move(dm));
+  }
+  HIPCHK(hipMemcpy(d_ch.p, ch.data(), sizeof(CfChain) * F, hipMemcpyHostToDevice));
   CfParams P{};
   P.n1 = (int)n1; P.D1 = (int)D1; P.n2 = (int)n2; P.D2 = (int)D2; P.r = (int)r; P.m = (int)m;
   P.rowsU = rowsU; P.rowsV = rowsV;
@@ -1462,63 +1504,94 @@ static int cf_sgd_run(
   P.epsw = epsw; P.epsU = epsU; P.langevin = langevin; P.stiefel = stiefel; P.seed = seed;
   P.fixw = fixw ? 1 : 0;
   P.uptr = d_up.as<int32_t>(); P.ufe = d_uf.as<int32_t>(); P.vptr = d_vp.as<int32_t>(); P.vfe = d_vf.as<int32_t>();
-  CfChain C{};
-  C.tr_user = d_tu.as<int32_t>(); C.tr_movie = d_tm.as<int32_t>(); C.tr_rating = d_tr.as<double>();
-  C.te_user = d_eu.as<int32_t>(); C.te_movie = d_em.as<int32_t>(); C.te_rating = d_er.as<double>();
-  C.N = (int)N; C.Ntest = (int)Ntest; C.perm = d_perm.as<int32_t>();
-  C.w = d_w.as<double>(); C.U = d_U.as<double>(); C.V = d_V.as<double>();
-  C.GU = d_GU.as<double>(); C.GV = d_GV.as<double>();
-  C.trainpred = d_trp.as<double>(); C.testpred = d_tep.as<double>(); C.sse = d_sse.as<double>();
-  C.status = d_st.as<int32_t>();
-  HIPCHK(hipMemcpy(d_ch.p, &C, sizeof(CfChain), hipMemcpyHostToDevice));
-  if (w_store) std::memset(w_store, 0, 8 * rr * maxepoch);
-  std::memset(U_store, 0, 8 * nU * maxepoch);
-  std::memset(V_store, 0, 8 * nV * maxepoch);
-  std::memset(testpred_store, 0, 8 * (size_t)Ntest * maxepoch);
-  std::memset(trainRMSE, 0, 8 * (size_t)maxepoch);
-  for (int64_t z = 0; z < maxepoch; ++z) testRMSE[z] = 10.0;              // :441
+  for (CfFold& fd : folds) {
+    if (fd.w_store) std::memset(fd.w_store, 0, 8 * rr * maxepoch);
+    std::memset(fd.U_store, 0, 8 * nU * maxepoch);
+    std::memset(fd.V_store, 0, 8 * nV * maxepoch);
+    std::memset(fd.testpred_store, 0, 8 * (size_t)fd.Ntest * maxepoch);
+    std::memset(fd.trainRMSE, 0, 8 * (size_t)maxepoch);
+    for (int64_t z = 0; z < maxepoch; ++z) fd.testRMSE[z] = 10.0;            // :441
+    fd.status = GPT_OK;
+  }
   std::vector<int32_t> perm(N);
-  std::vector<double> sse(2 * (size_t)neval), tp(Ntest);
-  int counter = 0, testcounter = 0;
-  for (int64_t epoch = 1; epoch <= burnin + maxepoch; ++epoch) {
+  std::vector<double> sse(2 * (size_t)neval), tp(ntmax);
+  std::vector<char> live(F, 1);
+  std::vector<int> testcounter(F, 0);
+  int counter = 0, nlive = F;
+  const int32_t stopped = 2;                         // skips the fold in later launches
+  for (int64_t epoch = 1; epoch <= burnin + maxepoch && nlive > 0; ++epoch) {
     host_randperm((int)N, seed, (int)(epoch - 1), perm.data());
     HIPCHK(hipMemcpy(d_perm.p, perm.data(), 4 * N, hipMemcpyHostToDevice));
-    hipError_t e = launch_cf_epoch(P, d_ch.as<CfChain>(), 1, (epoch - 1) * nbatch, nbatch, nullptr);
+    hipError_t e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, (epoch - 1) * nbatch, nbatch, nullptr);
     if (e != hipSuccess) return hip_fail(e, "cf epoch kernel");
-    int32_t bad = 0;
-    HIPCHK(hipMemcpy(&bad, d_st.p, 4, hipMemcpyDeviceToHost));
-    if (bad) {                       // :490-492 — zero parameter stores, curves as they are
-      if (w_store) std::memset(w_store, 0, 8 * rr * maxepoch);
-      std::memset(U_store, 0, 8 * nU * maxepoch);
-      std::memset(V_store, 0, 8 * nV * maxepoch);
+    for (int f = 0; f < F; ++f) {
+      if (!live[f]) continue;
+      int32_t bad = 0;
+      HIPCHK(hipMemcpy(&bad, d_st[f], 4, hipMemcpyDeviceToHost));
+      if (bad) {                     // :490-492 — zero parameter stores, curves as they are
+        CfFold& fd = folds[f];
+        if (fd.w_store) std::memset(fd.w_store, 0, 8 * rr * maxepoch);
+        std::memset(fd.U_store, 0, 8 * nU * maxepoch);
+        std::memset(fd.V_store, 0, 8 * nV * maxepoch);
+        fd.status = GPT_ERR_NAN_GEODESIC;
+        live[f] = 0; --nlive;
+      }
+    }
+    if (epoch > burnin && nlive > 0) {
+      const int64_t s2 = epoch - burnin - 1;
+      if (!avg) counter = 0;
+      e = launch_cf_eval(P, d_ch.as<CfChain>(), F, nmax, counter, nullptr);
+      if (e != hipSuccess) return hip_fail(e, "cf eval kernel");
+      for (int f = 0; f < F; ++f) {
+        if (!live[f]) continue;
+        CfFold& fd = folds[f];
+        if (fd.w_store) HIPCHK(hipMemcpy(fd.w_store + rr * s2, d_w[f], 8 * rr, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(fd.U_store + nU * s2, d_U[f], 8 * nU, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(fd.V_store + nV * s2, d_V[f], 8 * nV, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(sse.data(), d_sse[f], 16 * (size_t)neval, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(tp.data(), d_tep[f], 8 * fd.Ntest, hipMemcpyDeviceToHost));
+        double st0 = 0.0, st1 = 0.0;
+        for (int z = 0; z < neval; ++z) { st0 += sse[2 * z]; st1 += sse[2 * z + 1]; }
+        fd.trainRMSE[s2] = std::sqrt(st0 / (double)N);
+        fd.testRMSE[s2] = std::sqrt(st1 / (double)fd.Ntest);
+        for (int64_t i = 0; i < fd.Ntest; ++i)
+          fd.testpred_store[(size_t)fd.Ntest * s2 + i] =
+              std::min(std::max(tp[i] * fd.ystd + fd.ymean, 1.0), 5.0);
+        // :541-547 (the reference compares with the previous epoch's entry; none at s2 = 0)
+        if (epoch > 1 && s2 > 0 && fd.testRMSE[s2] > fd.testRMSE[s2 - 1]) testcounter[f] += 1;
+        else testcounter[f] = 0;
+        if (testcounter[f] >= 5) {
+          HIPCHK(hipMemcpy(d_st[f], &stopped, 4, hipMemcpyHostToDevice));
+          live[f] = 0; --nlive;
+        }
+      }
+      counter += 1;
+    }
+  }
+  for (const CfFold& fd : folds)
+    if (fd.status != GPT_OK) {
       set_error("Get NaN when moving along Geodesic. Try smaller epsU");
       return GPT_ERR_NAN_GEODESIC;
     }
-    if (epoch > burnin) {
-      const int64_t s2 = epoch - burnin - 1;
-      if (w_store) HIPCHK(hipMemcpy(w_store + rr * s2, d_w.p, 8 * rr, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(U_store + nU * s2, d_U.p, 8 * nU, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(V_store + nV * s2, d_V.p, 8 * nV, hipMemcpyDeviceToHost));
-      if (!avg) counter = 0;
-      e = launch_cf_eval(P, d_ch.as<CfChain>(), 1, (int)std::max(N, Ntest), counter, ytrainMean,
-                         ytrainStd, nullptr);
-      if (e != hipSuccess) return hip_fail(e, "cf eval kernel");
-      HIPCHK(hipMemcpy(sse.data(), d_sse.p, 16 * (size_t)neval, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(tp.data(), d_tep.p, 8 * Ntest, hipMemcpyDeviceToHost));
-      double st0 = 0.0, st1 = 0.0;
-      for (int z = 0; z < neval; ++z) { st0 += sse[2 * z]; st1 += sse[2 * z + 1]; }
-      trainRMSE[s2] = std::sqrt(st0 / (double)N);
-      testRMSE[s2] = std::sqrt(st1 / (double)Ntest);
-      for (int64_t i = 0; i < Ntest; ++i)
-        testpred_store[(size_t)Ntest * s2 + i] = std::min(std::max(tp[i] * ytrainStd + ytrainMean, 1.0), 5.0);
-      counter += 1;
-      // :541-547 (the reference compares with the previous epoch's entry; none at s2 = 0)
-      if (epoch > 1 && s2 > 0 && testRMSE[s2] > testRMSE[s2 - 1]) testcounter += 1;
-      else testcounter = 0;
-    }
-    if (testcounter >= 5) break;
-  }
   return GPT_OK;
+}
+
+// one fold (the reference functions' own signature)
+static int cf_sgd_one(const char* name, const double* Rating, int64_t N, int64_t ldr,
+                      const double* UserData, int64_t n1, int64_t D1, const double* MovieData,
+                      int64_t n2, int64_t D2, const double* Ratingtest, int64_t Ntest, int64_t ldt,
+                      double signal_var, double sigma_u, double sigma_w, const double* w_init,
+                      int64_t r, int64_t m, double epsw, double epsU, double a, double b, double c,
+                      int64_t burnin, int64_t maxepoch, uint64_t seed, double ytrainMean,
+                      double ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg, bool fixw,
+                      CfInit init, double* w_store, double* U_store, double* V_store,
+                      double* testpred_store, double* trainRMSE, double* testRMSE) {
+  std::vector<CfFold> folds(1);
+  folds[0] = CfFold{Rating, N, ldr, Ratingtest, Ntest, ldt, ytrainMean, ytrainStd, w_store, U_store,
+                    V_store, testpred_store, trainRMSE, testRMSE, GPT_OK};
+  return cf_sgd_run(name, folds, UserData, n1, D1, MovieData, n2, D2, signal_var, sigma_u, sigma_w,
+                    w_init, r, m, epsw, epsU, a, b, c, burnin, maxepoch, seed, langevin, stiefel,
+                    avg, fixw, init);
 }
 
 extern "C" int gpt_cf_fullw_sideinfo(
@@ -1529,11 +1602,38 @@ extern "C" int gpt_cf_fullw_sideinfo(
     int64_t maxepoch, uint64_t seed, double ytrainMean, double ytrainStd, int32_t langevin,
     int32_t stiefel, int32_t avg, double* w_store, double* U_store, double* V_store,
     double* testpred_store, double* trainRMSE, double* testRMSE) {
-  return cf_sgd_run("GPT_fullw_sideinfo", Rating, N, ldr, UserData, n1, D1, MovieData, n2, D2,
+  return cf_sgd_one("GPT_fullw_sideinfo", Rating, N, ldr, UserData, n1, D1, MovieData, n2, D2,
                     Ratingtest, Ntest, ldt, signal_var, sigma_u, sigma_w, w_init, r, m, epsw, epsU,
                     a, b, c, burnin, maxepoch, seed, ytrainMean, ytrainStd, langevin, stiefel, avg,
                     false, kCfInitSide, w_store, U_store, V_store, testpred_store, trainRMSE,
                     testRMSE);
+}
+
+extern "C" int gpt_cf_fullw_sideinfo_folds(
+    int64_t F, const double* const* Rating, const int64_t* N, const double* const* Ratingtest,
+    const int64_t* Ntest, const double* UserData, int64_t n1, int64_t D1, const double* MovieData,
+    int64_t n2, int64_t D2, double signal_var, double sigma_u, double sigma_w,
+    const double* w_init, int64_t r, int64_t m, double epsw, double epsU, double a, double b,
+    double c, int64_t burnin, int64_t maxepoch, uint64_t seed, const double* ytrainMean,
+    const double* ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg,
+    double* const* w_store, double* const* U_store, double* const* V_store,
+    double* const* testpred_store, double* const* trainRMSE, double* const* testRMSE,
+    int32_t* status) {
+  if (F < 1 || F > 65535 || !Rating || !N || !Ratingtest || !Ntest || !ytrainMean || !ytrainStd ||
+      !w_store || !U_store || !V_store || !testpred_store || !trainRMSE || !testRMSE) {
+    set_error("bad GPT_fullw_sideinfo_folds arguments"); return GPT_ERR_BAD_DIMS;
+  }
+  std::vector<CfFold> folds(F);
+  for (int64_t f = 0; f < F; ++f)
+    folds[f] = CfFold{Rating[f], N[f], N[f], Ratingtest[f], Ntest[f], Ntest[f], ytrainMean[f],
+                      ytrainStd[f], w_store[f], U_store[f], V_store[f], testpred_store[f],
+                      trainRMSE[f], testRMSE[f], GPT_OK};
+  const int rc = cf_sgd_run("GPT_fullw_sideinfo_folds", folds, UserData, n1, D1, MovieData, n2, D2,
+                            signal_var, sigma_u, sigma_w, w_init, r, m, epsw, epsU, a, b, c,
+                            burnin, maxepoch, seed, langevin, stiefel, avg, false, kCfInitSide);
+  if (status)
+    for (int64_t f = 0; f < F; ++f) status[f] = folds[f].status;
+  return rc;
 }
 
 extern "C" int gpt_cf_fixw_sideinfo(
@@ -1544,7 +1644,7 @@ extern "C" int gpt_cf_fixw_sideinfo(
     double ytrainMean, double ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg,
     double* U_store, double* V_store, double* testpred_store, double* trainRMSE,
     double* testRMSE) {
-  return cf_sgd_run("GPT_fixw_sideinfo", Rating, N, ldr, UserData, n1, D1, MovieData, n2, D2,
+  return cf_sgd_one("GPT_fixw_sideinfo", Rating, N, ldr, UserData, n1, D1, MovieData, n2, D2,
                     Ratingtest, Ntest, ldt, signal_var, sigma_u, 1.0, w, r, m, 0.0, epsU, a, b, c,
                     burnin, maxepoch, seed, ytrainMean, ytrainStd, langevin, stiefel, avg, true,
                     kCfInitSigma, nullptr, U_store, V_store, testpred_store, trainRMSE, testRMSE);
@@ -1558,7 +1658,7 @@ extern "C" int gpt_cf_fullw(const double* Rating, int64_t N, int64_t ldr, int64_
                             double ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg,
                             double* w_store, double* U_store, double* V_store,
                             double* testpred_store, double* trainRMSE, double* testRMSE) {
-  return cf_sgd_run("GPT_fullw", Rating, N, ldr, nullptr, n1, 0, nullptr, n2, 0, Ratingtest,
+  return cf_sgd_one("GPT_fullw", Rating, N, ldr, nullptr, n1, 0, nullptr, n2, 0, Ratingtest,
                     Ntest, ldt, signal_var, sigma_u, sigma_w, w_init, r, m, epsw, epsU, 1.0, 0.0,
                     0.0, burnin, maxepoch, seed, ytrainMean, ytrainStd, langevin, stiefel, avg,
                     false, kCfInitUnit, w_store, U_store, V_store, testpred_store, trainRMSE,
@@ -1572,7 +1672,7 @@ extern "C" int gpt_cf_fixw(const double* Rating, int64_t N, int64_t ldr, int64_t
                            double ytrainStd, int32_t langevin, int32_t stiefel, int32_t avg,
                            double* U_store, double* V_store, double* testpred_store,
                            double* trainRMSE, double* testRMSE) {
-  return cf_sgd_run("GPT_fixw", Rating, N, ldr, nullptr, n1, 0, nullptr, n2, 0, Ratingtest, Ntest,
+  return cf_sgd_one("GPT_fixw", Rating, N, ldr, nullptr, n1, 0, nullptr, n2, 0, Ratingtest, Ntest,
                     ldt, signal_var, sigma_u, 1.0, w, r, m, 0.0, epsU, 1.0, 0.0, 0.0, burnin,
                     maxepoch, seed, ytrainMean, ytrainStd, langevin, stiefel, avg, true,
                     kCfInitSigma, nullptr, U_store, V_store, testpred_store, trainRMSE, testRMSE);
@@ -1714,6 +1814,7 @@ static int cf_gibbs_run(
   Cc.N = (int)N; Cc.Ntest = (int)Ntest; Cc.w = d_w.as<double>(); Cc.U = d_U.as<double>();
   Cc.V = d_V.as<double>(); Cc.trainpred = d_trp.as<double>(); Cc.testpred = d_tep.as<double>();
   Cc.sse = d_sse.as<double>(); Cc.status = d_st.as<int32_t>();
+  Cc.ymean = ytrainMean; Cc.ystd = ytrainStd;
   HIPCHK(hipMemcpy(d_ch.p, &Cc, sizeof(CfChain), hipMemcpyHostToDevice));
   if (w_store) std::memset(w_store, 0, 8 * rr * maxepoch);
   std::memset(U_store, 0, 8 * nU * maxepoch);
@@ -1756,7 +1857,7 @@ static int cf_gibbs_run(
       HIPCHK(hipMemcpy(V_store + nV * s2, d_V.p, 8 * nV, hipMemcpyDeviceToHost));
       if (!avg) counter = 0;
       hipError_t e = launch_cf_eval(P, d_ch.as<CfChain>(), 1, (int)std::max(N, Ntest), counter,
-                                    ytrainMean, ytrainStd, nullptr);
+                                    nullptr);
       if (e != hipSuccess) return hip_fail(e, "cf eval kernel");
       HIPCHK(hipMemcpy(sse.data(), d_sse.p, 16 * (size_t)neval, hipMemcpyDeviceToHost));
       HIPCHK(hipMemcpy(tp.data(), d_tep.p, 8 * Ntest, hipMemcpyDeviceToHost));

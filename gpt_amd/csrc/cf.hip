@@ -306,10 +306,12 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
 // (:526-529, :536-539), de-standardised and cut off, squared error summed per block into
 // C.sse[2·blockIdx.x + set] (the host adds the partials in order).
 template <int R>
-__global__ __launch_bounds__(256) void cf_eval_kernel(CfParams P, const CfChain* chains, int counter,
-                                                      double ymean, double ystd) {
+__global__ __launch_bounds__(256) void cf_eval_kernel(CfParams P, const CfChain* chains, int counter) {
   __shared__ double red[4];
   const CfChain C = chains[blockIdx.z];
+  // a stopped (early stop) or bailed-out fold keeps its last predictions
+  if (__hip_atomic_load(C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  const double ymean = C.ymean, ystd = C.ystd;
   const int set = blockIdx.y;
   const int n = set ? C.Ntest : C.N;
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -534,13 +536,12 @@ hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains
 }
 
 hipError_t launch_cf_eval(const CfParams& P, const CfChain* chains, int nchains, int nmax,
-                          int counter, double ymean, double ystd, hipStream_t st) {
+                          int counter, hipStream_t st) {
   dim3 grid((unsigned)((nmax + 255) / 256), 2, nchains);
   switch (P.r) {
 #define CASE(RR)                                                                              \
   case RR:                                                                                    \
-    hipLaunchKernelGGL(cf_eval_kernel<RR>, grid, dim3(256), 0, st, P, chains, counter, ymean, \
-                       ystd);                                                                 \
+    hipLaunchKernelGGL(cf_eval_kernel<RR>, grid, dim3(256), 0, st, P, chains, counter);        \
     break;
     GPT_CF_RANKS(CASE)
 #undef CASE

@@ -211,6 +211,7 @@ struct CfChain {
   double* V;                // rowsV*r
   double* GU;               // rowsU*r zeroed scratch (gradient rows / momentum)
   double* GV;
+  double ymean, ystd;       // ytrainMean / ytrainStd of the chain's fold (evaluation)
   double* trainpred;        // N      running averages (avg)
   double* testpred;         // Ntest
   double* sse;              // 2 * gridDim.x partial sums of the eval kernel
@@ -222,7 +223,7 @@ bool cf_rank_supported(int r);
 hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
                            int nb, hipStream_t st);
 hipError_t launch_cf_eval(const CfParams& P, const CfChain* chains, int nchains, int nmax,
-                          int counter, double ymean, double ystd, hipStream_t st);
+                          int counter, hipStream_t st);
 hipError_t launch_cfg_rows(int side, int r, const double* W, const double* Oth, int rows_oth,
                            double* Me, int rows_me, const int32_t* ptr, const int32_t* lst,
                            const int32_t* other, const double* y, double signal_var, double su2,

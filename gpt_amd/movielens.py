@@ -8,6 +8,9 @@ BASELINE config 5) on libgptsgld.so.
     GPT_fullw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, sigma_w,
                     w_init, burnin, maxepoch, n_samples, param_seed, ytrainMean, ytrainStd;
                     avg=False, rotated_w=False)              100k_movielensExperiment.jl:1032-1129
+    GPT_fullw_sideinfo_folds(Ratings, UserData, MovieData, Ratingtests, ..., ytrainMeans,
+                             ytrainStds; ...)   the folds loop of :733-736 as one device launch
+                                                per epoch (a list of per-fold result tuples)
     GPT_fixw_sideinfo(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u, w, m, epsU,
                       a, b, c, burnin, maxepoch, param_seed, ytrainMean, ytrainStd;
                       langevin, stiefel, avg)                  :282-404
@@ -26,12 +29,14 @@ testpred_store, trainRMSEvec, testRMSEvec), without w_store for the fixed-w vari
 scripts/make_ml100k_fixture.py (ratings per fold, the processed UserData / MovieData of
 :578-584).  Randomness follows the framework's Philox contract (oracle/movielens_ref.py).
 """
+import ctypes as C
+
 import numpy as np
 
 from ._lib import P_D, check, lib
 from . import _lib
 
-__all__ = ["GPT_fullw_sideinfo", "GPT_fixw_sideinfo", "GPT_fullw", "GPT_fixw", "GPT_fullw_gibbs",
+__all__ = ["GPT_fullw_sideinfo", "GPT_fullw_sideinfo_folds", "GPT_fixw_sideinfo", "GPT_fullw", "GPT_fixw", "GPT_fullw_gibbs",
            "GPT_fixw_gibbs", "fold"]
 
 
@@ -205,3 +210,47 @@ def GPT_fixw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u,
         int(bool(avg)), int(bool(rotated_w)), _ptr(U_store), _ptr(V_store), _ptr(tps), _ptr(trm),
         _ptr(tsm)))
     return U_store, V_store, tps, trm, tsm
+
+
+def GPT_fullw_sideinfo_folds(Ratings, UserData, MovieData, Ratingtests, signal_var, sigma_u,
+                             sigma_w, w_init, m, epsw, epsU, a, b, c, burnin, maxepoch, param_seed,
+                             ytrainMeans, ytrainStds, langevin=False, stiefel=False, avg=False):
+    """The per-fold loop of 100k_movielensExperiment.jl:733-736 (GPT_fullw_sideinfo on fold i
+    with its own ratings and ytrainMean[i] / ytrainStd[i], one param_seed) with the folds as
+    sibling chains of one device launch per epoch.  Returns one (w_store, U_store, V_store,
+    testpred_store, trainRMSEvec, testRMSEvec) tuple per fold — the same values as separate
+    GPT_fullw_sideinfo calls; a fold that hit the geodesic NaN keeps zero parameter stores."""
+    F = len(Ratings)
+    if len(Ratingtests) != F or len(ytrainMeans) != F or len(ytrainStds) != F:
+        raise ValueError("one test set, ytrainMean and ytrainStd per fold")
+    Rts = [_f64(R) for R in Ratings]
+    Rss = [_f64(R) for R in Ratingtests]
+    Ud, Md, w0 = _f64(UserData), _f64(MovieData), _f64(w_init)
+    n1, D1 = Ud.shape
+    n2, D2 = Md.shape
+    r = w0.shape[0]
+    outs = []
+    for Rs in Rss:
+        outs.append((np.zeros((r, r, maxepoch), order="F"),
+                     np.zeros((n1 + D1, r, maxepoch), order="F"),
+                     np.zeros((n2 + D2, r, maxepoch), order="F"),
+                     np.zeros((Rs.shape[0], maxepoch), order="F"), np.zeros(maxepoch),
+                     np.zeros(maxepoch)))
+    PP = C.c_void_p * F
+    ptrs = lambda arrs: PP(*[a.ctypes.data for a in arrs])
+    Ns = np.array([R.shape[0] for R in Rts], dtype=np.int64)
+    Nts = np.array([R.shape[0] for R in Rss], dtype=np.int64)
+    ym = _f64(np.asarray(ytrainMeans, dtype=np.float64))
+    ys = _f64(np.asarray(ytrainStds, dtype=np.float64))
+    st = np.zeros(F, dtype=np.int32)
+    code = lib().gpt_cf_fullw_sideinfo_folds(
+        F, ptrs(Rts), Ns.ctypes.data, ptrs(Rss), Nts.ctypes.data, _ptr(Ud), n1, D1, _ptr(Md), n2,
+        D2, float(signal_var), float(sigma_u), float(sigma_w), _ptr(w0), r, int(m), float(epsw),
+        float(epsU), float(a), float(b), float(c), int(burnin), int(maxepoch),
+        int(param_seed) & (2 ** 64 - 1), _ptr(ym), _ptr(ys), int(bool(langevin)),
+        int(bool(stiefel)), int(bool(avg)), ptrs([o[0] for o in outs]),
+        ptrs([o[1] for o in outs]), ptrs([o[2] for o in outs]), ptrs([o[3] for o in outs]),
+        ptrs([o[4] for o in outs]), ptrs([o[5] for o in outs]),
+        st.ctypes.data_as(_lib.P_I32))
+    _nan_or_check(code)
+    return outs

@@ -113,6 +113,12 @@ class SGLDSession:
                                                   C.c_void_p(w_out.data_ptr()),
                                                   C.c_void_p(U_out.data_ptr())))
 
+    def status(self, chain):
+        """GPT_OK, or GPT_ERR_NAN_GEODESIC when chain hit the geodesic bail-out (4 bytes copied)."""
+        st = C.c_int32(0)
+        check(lib().gpt_sgld_session_fetch(self._h, chain, None, None, None, C.byref(st)))
+        return st.value
+
     def fetch(self, chain, diag=False):
         """(w_store, U_store, status[, diag]) of one chain, host numpy in Julia layout."""
         ws = np.zeros((self.Q, self.nstore), order="F")

@@ -253,6 +253,27 @@ int gpt_cf_fullw_gibbs(const double* Rating, int64_t N, int64_t ldr, int64_t n1,
                        double* w_store, double* U_store, double* V_store, double* testpred_store,
                        double* trainRMSE, double* testRMSE);
 
+/* The folds of 100k_movielensExperiment.jl:733-736 (`@parallel for i=1:5` over
+ * GPT_fullw_sideinfo(Ratingtrain[:,:,i], ..., Ratingtest[:,:,i], ..., ytrainMean[i],
+ * ytrainStd[i])) as F sibling chains of one device launch per epoch: fold f reads Rating[f]
+ * (N[f] x >=3, column-major, leading dimension N[f]) and Ratingtest[f] (Ntest[f] x >=3) and
+ * writes w_store[f] .. testRMSE[f] exactly as F separate gpt_cf_fullw_sideinfo calls with the
+ * same param_seed would (same init, per-epoch permutation and early stop, per fold); every fold
+ * has the same N.  status[f] (optional): GPT_OK or GPT_ERR_NAN_GEODESIC for that fold; the return
+ * value is GPT_ERR_NAN_GEODESIC when any fold bailed out. */
+int gpt_cf_fullw_sideinfo_folds(int64_t F, const double* const* Rating, const int64_t* N,
+                                const double* const* Ratingtest, const int64_t* Ntest,
+                                const double* UserData, int64_t n1, int64_t D1,
+                                const double* MovieData, int64_t n2, int64_t D2, double signal_var,
+                                double sigma_u, double sigma_w, const double* w_init, int64_t r,
+                                int64_t m, double epsw, double epsU, double a, double b, double c,
+                                int64_t burnin, int64_t maxepoch, uint64_t seed,
+                                const double* ytrainMean, const double* ytrainStd,
+                                int32_t langevin, int32_t stiefel, int32_t avg,
+                                double* const* w_store, double* const* U_store,
+                                double* const* V_store, double* const* testpred_store,
+                                double* const* trainRMSE, double* const* testRMSE, int32_t* status);
+
 /* The other SGD / SGLD variants of the CF model (same Rating / Ratingtest / output conventions
  * as gpt_cf_fullw_sideinfo; the NaN bail-out zeroes the parameter stores):
  *   GPT_fixw_sideinfo(Rating,UserData,MovieData,Ratingtest,signal_var,sigma_u,w,m,epsU,a,b,c,

@@ -172,3 +172,30 @@ def test_fixw_gibbs_matches_oracle(rotated):
     for g, w_ in zip(got[:2], want[:2]):
         assert rel(g, w_) < 1e-8, rel(g, w_)
     _check_tail(got, want)
+
+
+@pytest.mark.parametrize("lang,stf,avg", [(False, False, False), (True, True, True)])
+def test_sideinfo_folds_equal_separate_runs(lang, stf, avg):
+    """The folds loop of :733-736 as one launch per epoch (gpt_cf_fullw_sideinfo_folds) gives
+    every fold exactly the values of its own GPT_fullw_sideinfo call (bit-identical: the same
+    kernels, one chain per fold)."""
+    from gpt_amd import movielens
+    d = np.load(GOLD)
+    folds = [movielens.fold(d, i) for i in (1, 2, 3)]
+    trs = [f[0][:3000] for f in folds]
+    tes = [f[1][:700 + 50 * i] for i, f in enumerate(folds)]       # test sets of different sizes
+    ud, md = folds[0][2], folds[0][3]
+    mus = [f[4] for f in folds]
+    sds = [f[5] for f in folds]
+    w0 = np.random.default_rng(5).standard_normal((4, 4))
+    epsU = 1e-4 if stf else 1e-6
+    common = (0.8, 0.1, 1.0, w0, 100, 1e-4, epsU, 0.5, 0.25, 0.5, 0, 3, 17)
+    got = movielens.GPT_fullw_sideinfo_folds(trs, ud, md, tes, *common, mus, sds, langevin=lang,
+                                             stiefel=stf, avg=avg)
+    assert len(got) == 3
+    for f in range(3):
+        want = movielens.GPT_fullw_sideinfo(trs[f], ud, md, tes[f], *common, mus[f], sds[f],
+                                            langevin=lang, stiefel=stf, avg=avg)
+        for g, w_ in zip(got[f], want):
+            assert g.shape == w_.shape
+            assert np.array_equal(g, w_)

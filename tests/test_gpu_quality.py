@@ -66,7 +66,7 @@ def test_kin40k_reference_configuration_tracks_reference_curve():
     ref = np.load(os.path.join(ROOT, "tests", "golden", "ref_curves.npz"))["testRMSE_kin40k"]
     curves, alive = [], 0
     for c in range(sweeps):
-        if sess.fetch(c)[2] != 0:                               # NaN bail-out: zero stores
+        if sess.status(c) != 0:                               # NaN bail-out: zero stores
             continue
         alive += 1
         _, _, ws, Us, ns = sess.device_state(c)
