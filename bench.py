@@ -373,6 +373,9 @@ def main():
     torch.cuda.synchronize()
     pred_ms = ev0.elapsed_time(ev1)
     pred_flop = 2.0 * npred * r * n * D * Nte             # the GEMM (dominant); V-phase excluded
+    from gpt_amd.session import pred_device_timed
+    gemm_ms, vphase_ms = pred_device_timed(w_all.data_ptr(), U_all.data_ptr(), I0, phi_te, n, D,
+                                           Nte, r, Q, npred, fh)
     fsum = fh.sum(dim=0)
     combine_predictive_mean(torch.zeros_like(fsum), 1)   # warm-up (communicator setup, kernels)
     torch.cuda.synchronize()
@@ -448,6 +451,10 @@ def main():
                      "frac": pred_flop / (pred_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS,
                      "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + pred_vphase_kernel",
                      "note": "whole stacked-sample call timed with events (GEMM + V-phase)",
+                     "gemm_ms": gemm_ms, "vphase_ms": vphase_ms,
+                     "gemm_roofline": {"bound": "mfma", "achieved": pred_flop / (gemm_ms * 1e-3) / 1e12,
+                                       "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                       "frac": pred_flop / (gemm_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS},
                      "final_state_ensemble_rmse": rmse_final},
             "single_chain": single,
             "single_chain_steps_per_s": single["steps_per_s"] if single else None,

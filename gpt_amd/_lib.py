@@ -73,6 +73,9 @@ SIGNATURES = {
     "gpt_pred_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_void_p,
                                C.c_void_p]),
+    "gpt_pred_dev_timed": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                     C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                     C.c_void_p, C.c_void_p, P_D]),
     "gpt_pred_mean": (C.c_int, [P_D, P_D, P_I32, P_D, P_D, C.c_int64, C.c_int64, C.c_int64,
                                 C.c_int64, C.c_int64, C.c_int64, C.c_double, P_D, P_D]),
     "gpt_gpnt_sgld": (C.c_int, [P_D, P_D, C.c_int64, C.c_int64, C.c_double, C.c_double, C.c_int64,

@@ -1062,6 +1062,22 @@ extern "C" int gpt_pred_dev(const double* w_dev, const double* U_dev, const int3
   return GPT_OK;
 }
 
+extern "C" int gpt_pred_dev_timed(const double* w_dev, const double* U_dev, const int32_t* I0_dev,
+                                  const double* phitest_dev, int64_t n, int64_t D, int64_t Ntest,
+                                  int64_t r, int64_t Q, int64_t S, double* fhat_dev,
+                                  void* hip_stream, double* ms_out) {
+  if (!valid_pred(n, D, Ntest, r, Q)) return GPT_ERR_BAD_DIMS;
+  if (!ms_out) { set_error("gpt_pred_dev_timed: ms_out is null"); return GPT_ERR_BAD_DIMS; }
+  PredPhaseTiming tm;
+  hipError_t e = launch_pred(w_dev, U_dev, I0_dev, phitest_dev, (int)n, (int)D, Ntest, (int)r,
+                             (int)Q, (int)S, fhat_dev, (hipStream_t)hip_stream, &tm);
+  if (e != hipSuccess) return hip_fail(e, "pred kernel");
+  HIPCHK(hipStreamSynchronize((hipStream_t)hip_stream));
+  ms_out[0] = tm.gemm_ms;
+  ms_out[1] = tm.vphase_ms;
+  return GPT_OK;
+}
+
 static int pred_host(const double* w, const double* U, const int32_t* I, const double* phitest,
                      const double* ytest, int64_t n, int64_t D, int64_t Ntest, int64_t r,
                      int64_t Q, int64_t S, double scale, double* fhat_out, double* mean_out,

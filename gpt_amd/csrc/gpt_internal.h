@@ -174,9 +174,12 @@ hipError_t launch_pred_x(const double* w, const double* U, const int32_t* I0, co
                          const double* ls, const double* Z, const double* bfe, double c, int n,
                          int D, long long Ntest, int r, int Q, int S, double* fhat, hipStream_t st);
 size_t pred_x_lds_bytes(int n, int D, int r, int Q);
+// Per-phase event timing of the stacked-sample prediction (diagnostics / the benchmark):
+// gemm_ms / vphase_ms accumulate over the sample chunks of one call.
+struct PredPhaseTiming { double gemm_ms = 0.0, vphase_ms = 0.0; };
 hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, const double* phitest,
                        int n, int D, long long Ntest, int r, int Q, int S, double* fhat,
-                       hipStream_t st);
+                       hipStream_t st, PredPhaseTiming* timing = nullptr);
 hipError_t launch_mean_rmse(const double* fhat, const double* ytest, long long Ntest, int S,
                             double* mean_out, double* sse_out, hipStream_t st);
 hipError_t launch_feature(const double* X, long long N, int D, const double* ls, double c,

@@ -435,7 +435,14 @@ static hipError_t launch_pred_gemm(const double* Us, const double* phitest, int 
 
 static hipError_t launch_pred_mfma(const double* w, const double* U, const int32_t* I0,
                                    const double* phitest, int n, int D, long long Ntest, int r,
-                                   int Q, int S, double* fhat, hipStream_t st) {
+                                   int Q, int S, double* fhat, hipStream_t st,
+                                   PredPhaseTiming* timing) {
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  if (timing)
+    for (auto& x : ev) {
+      const hipError_t ee = hipEventCreate(&x);
+      if (ee != hipSuccess) return ee;
+    }
   // temp of up to ~2 GiB of samples per pass; a pass of several workgroup tiles takes a multiple of
   // 128 / gcd(128, r) samples, so its S·r columns fill whole 128-column tiles (no MFMA padding)
   const size_t per_sample = 8 * (size_t)D * r * (size_t)Ntest;
@@ -462,8 +469,10 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
   for (int s0 = 0; s0 < S && e == hipSuccess; s0 += chunk) {
     const int Sc = std::min(chunk, S - s0);
     const double* Us = U + (size_t)s0 * n * r * D;
+    if (timing) (void)hipEventRecord(ev[0], st);
     e = launch_pred_gemm(Us, phitest, n, D, r, Ntest, Sc, T, st);
     if (e != hipSuccess) break;
+    if (timing) (void)hipEventRecord(ev[1], st);
     dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
     if (!tile_vphase) {
       if (rlds > 64 * 1024) {
@@ -474,6 +483,15 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
       hipLaunchKernelGGL(pred_vphase_rows_kernel, vg, dim3(64), rlds, st, w + (size_t)s0 * Q, T,
                          offs, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest);
       e = hipGetLastError();
+      if (timing && e == hipSuccess) {
+        (void)hipEventRecord(ev[2], st);
+        (void)hipEventSynchronize(ev[2]);
+        float a = 0.f, b = 0.f;
+        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+        (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+        timing->gemm_ms += a;
+        timing->vphase_ms += b;
+      }
       continue;
     }
     switch (r) {
@@ -492,6 +510,8 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     }
   }
   hipError_t ef = hipFreeAsync(T, st);
+  if (timing)
+    for (auto& x : ev) (void)hipEventDestroy(x);
   return e != hipSuccess ? e : ef;
 }
 
@@ -521,14 +541,14 @@ static hipError_t launch_pred_direct(const double* w, const double* U, const int
 // GPTSGLD_PRED=direct selects the per-sample streaming kernel (pred_kernel) for comparison.
 hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, const double* phitest,
                        int n, int D, long long Ntest, int r, int Q, int S, double* fhat,
-                       hipStream_t st) {
+                       hipStream_t st, PredPhaseTiming* timing) {
   if (Ntest <= 0 || S <= 0) return hipSuccess;
   static const bool direct = [] {
     const char* ev = std::getenv("GPTSGLD_PRED");
     return ev && std::strcmp(ev, "direct") == 0;
   }();
   if (direct) return launch_pred_direct(w, U, I0, phitest, n, D, Ntest, r, Q, S, fhat, st);
-  return launch_pred_mfma(w, U, I0, phitest, n, D, Ntest, r, Q, S, fhat, st);
+  return launch_pred_mfma(w, U, I0, phitest, n, D, Ntest, r, Q, S, fhat, st, timing);
 }
 
 hipError_t launch_pred_x(const double* w, const double* U, const int32_t* I0, const double* X,

@@ -157,6 +157,16 @@ def feature_device(X, length_scale, sigma_RBF, phi_scale, Z, b, stream=None):
     return phi
 
 
+def pred_device_timed(w_ptr, U_ptr, I0_dev, phitest, n, D, Ntest, r, Q, S, fhat_out):
+    """pred_device on the null stream with per-phase event timing: (gemm_ms, vphase_ms)."""
+    ms = np.zeros(2)
+    check(lib().gpt_pred_dev_timed(C.c_void_p(w_ptr), C.c_void_p(U_ptr),
+                                   C.c_void_p(I0_dev.data_ptr()), C.c_void_p(phitest.data_ptr()),
+                                   n, D, Ntest, r, Q, S, C.c_void_p(fhat_out.data_ptr()), None,
+                                   ms.ctypes.data_as(_lib.P_D)))
+    return float(ms[0]), float(ms[1])
+
+
 def pred_device(w_ptr, U_ptr, I0_dev, phitest, n, D, Ntest, r, Q, S, fhat_out, stream=None):
     """fhat (Ntest, S) on the device from S consecutive samples at w_ptr / U_ptr."""
     check(lib().gpt_pred_dev(C.c_void_p(w_ptr), C.c_void_p(U_ptr), C.c_void_p(I0_dev.data_ptr()),

@@ -171,6 +171,12 @@ int gpt_pred(const double* w, const double* U, const int32_t* I, const double* p
 int gpt_pred_dev(const double* w_dev, const double* U_dev, const int32_t* I0_dev,
                  const double* phitest_dev, int64_t n, int64_t D, int64_t Ntest, int64_t r,
                  int64_t Q, int64_t S, double* fhat_dev, void* hip_stream);
+/* gpt_pred_dev with per-phase event timing (diagnostics / the benchmark): ms_out[0] = the
+ * phidotU GEMM (fp64 MFMA) kernels, ms_out[1] = the V-phase kernels, summed over the sample
+ * chunks of the call; synchronises hip_stream. */
+int gpt_pred_dev_timed(const double* w_dev, const double* U_dev, const int32_t* I0_dev,
+                       const double* phitest_dev, int64_t n, int64_t D, int64_t Ntest, int64_t r,
+                       int64_t Q, int64_t S, double* fhat_dev, void* hip_stream, double* ms_out);
 /* Posterior-mean prediction over S samples + RMSE (GPT_SGLD_p.jl:124-132,
  * kin40kExperiment.jl:80-87): mean_out (Ntest), returns rmse*scale in *rmse_out. */
 int gpt_pred_mean(const double* w_store, const double* U_store, const int32_t* I,
