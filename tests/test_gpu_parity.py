@@ -162,12 +162,18 @@ CASES = {
     "c2_n258_thin": (258, 6, 60, 4, 130, 15, 1, 2, 3, True, True),      # 2 rows in the second half
     "c2_n512_q256": (512, 8, 70, 5, 256, 33, 0, 1, 1, True, True),      # full halves, 8 V tasks, odd m
     "c2_r2_d7": (300, 7, 64, 2, 100, 16, 0, 2, 2, True, True),
+    # edge shapes: a last batch of one row (an odd row group), one input dimension, odd n with
+    # one 64-row block (4-B row staging), odd n past one block (the chain engine declines: grid)
+    "last_row_alone": (24, 2, 41, 2, 4, 8, 0, 2, 1, True, True),
+    "d1": (32, 1, 30, 3, 3, 7, 0, 2, 1, True, True),
+    "n17_odd": (17, 3, 40, 2, 6, 8, 0, 2, 1, True, True),
+    "n101_odd": (101, 2, 33, 3, 9, 10, 0, 2, 1, True, True),
 }
 
 
 def _chain_ok(n, D, r, lang, stf):
     """Shapes the chain engine (chain.hip) takes; the grid engine (sgld.hip) takes all."""
-    return lang and stf and D <= 8 and r <= 5 and n <= 512
+    return lang and stf and D <= 8 and r <= 5 and n <= 512 and (n <= 64 or n % 2 == 0)
 
 
 def _shape(name):
@@ -459,3 +465,14 @@ def test_epoch_order_ring_over_many_epochs(engine):
                                    store_every=2)
     assert info["status"] == 0
     assert rel(got_w, wo) < 1e-8 and rel(got_U, Uo) < 1e-8
+
+
+def test_chain_engine_declines_odd_n_past_one_block():
+    """Odd n > 64 cannot use the chain engine's 16-B row staging: forcing it fails loudly
+    (GPT_ERR_BAD_DIMS) and the default selection runs the grid engine (n101_odd above)."""
+    from gpt_amd._lib import GPTError
+    n, D, N, r, Q, m, burnin, maxepoch, se, lang, stf = CASES["n101_odd"]
+    p = make_problem(n, D, N, r, Q, seed=11)
+    with pytest.raises(GPTError):
+        G().GPTregression(p["phi"], p["y"], 0.05, p["I"], r, Q, m, 1e-4, 1e-6, burnin, maxepoch,
+                          23, store_every=se, engine="chain")
