@@ -35,6 +35,9 @@ namespace gpt {
 #ifndef CHAIN_TOUCH               // next-batch rows pulled into L2 / Infinity Cache during the
 #define CHAIN_TOUCH 0             // Stiefel phase (rows per dimension; 0 = off)
 #endif
+#ifndef CHAIN_BFLY
+#define CHAIN_BFLY 1              // (b) reduction: register butterfly (1) or LDS scratch + 8-lane DPP (0)
+#endif
 #ifndef CHAIN_STAGE_AT
 #define CHAIN_STAGE_AT 3          // next group's rows staged at: 0 (a), 1 (c), 2 (e), 3 end of (b), 4 end of (c)
 #endif
@@ -335,6 +338,30 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     // wave's LDS scratch by 8-lane groups (lane 8l+s sums 8 partials of output l, DPP finishes)
     double* tsl = temp_l + slot * L::TS;
     const int rl = min(ln >> 3, R - 1), rs = ln & 7;
+#if CHAIN_BFLY
+    {
+      // the G·R partial dots of this lane, reduced over the wave by one register butterfly
+      // (permlane swaps + DPP, no LDS round trip): lane λ ends with the total of value λ >> SH
+      constexpr int NVB = G * R <= 8 ? 8 : (G * R <= 16 ? 16 : (G * R <= 32 ? 32 : 64));
+      constexpr int SH = 6 - Butterfly<NVB>::P;
+      double v[NVB];
+#pragma unroll
+      for (int x = 0; x < NVB; ++x) v[x] = 0.0;
+#pragma unroll
+      for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+        for (int jj = 0; jj < J; ++jj)
+#pragma unroll
+          for (int l = 0; l < R; ++l) v[gg * R + l] = fma(p[gg][jj], u[jj][l], v[gg * R + l]);
+      Butterfly<NVB>::run(v, ln);
+      const int vi = ln >> SH;
+      if ((ln & ((1 << SH) - 1)) == 0 && vi < G * R) {
+        const int gg = vi / R, l = vi - gg * R;
+        tsl[(k * R + l) * G + gg] = v[0];
+        tsl[DRG + G + (k * R + l) * G + gg] = rcp_nr(v[0]);
+      }
+    }
+#else
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
       double v[R];
@@ -363,6 +390,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         tsl[DRG + G + (k * R + rl) * G + gg] = rcp_nr(sv);
       }
     }
+#endif
 #if CHAIN_STAGE_AT == 3 && !CHAIN_DBUF
     if (!CHAIN_EXP_NOSTAGE && g0 + G < Bt) stage(g0 + G, ln, pw);
 #endif
