@@ -449,7 +449,7 @@ def main():
                      "achieved_tflops": pred_flop / (pred_ms * 1e-3) / 1e12,
                      "peak_tflops": FP64_MFMA_PEAK_TFS,
                      "frac": pred_flop / (pred_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS,
-                     "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + pred_vphase_kernel",
+                     "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + pred_vphase_pairs_kernel",
                      "note": "whole stacked-sample call timed with events (GEMM + V-phase)",
                      "gemm_ms": gemm_ms, "vphase_ms": vphase_ms,
                      "gemm_roofline": {"bound": "mfma", "achieved": pred_flop / (gemm_ms * 1e-3) / 1e12,

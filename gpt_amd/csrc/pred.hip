@@ -401,6 +401,102 @@ __global__ __launch_bounds__(64) void pred_vphase_rows_kernel(const double* __re
   if (ok) fhat[(size_t)s * Ntest + i] = f0 + f1;
 }
 
+// V-phase with pair tables: the D factors of V[q, i] are taken two dimensions at a time from
+// per-test-row tables PP_t[a·r + b] = temp[2t, a]·temp[2t+1, b] (an odd last dimension keeps its r
+// rows), built once per (sample, 64 rows) workgroup, so a core entry costs ⌈D/2⌉ lane-contiguous LDS
+// reads instead of D — the rows kernel above is bound by exactly those reads (64 lanes × 8 B at
+// 128 B/clk per CU).  Four waves split the core entries; their partial sums are added in wave
+// order.  V = Π_t PP_t associates the D factors pairwise (the oracle multiplies them in k order):
+// the two differ by rounding only.
+constexpr int kPairWaves = 4;
+static int pred_pair_tables(int D) { return (D + 1) / 2; }
+static int pred_pair_rows(int D, int r) { return (D / 2) * r * r + (D & 1) * r; }
+static size_t pred_pairs_lds_bytes(int D, int r) {
+  return 8 * (size_t)pred_pair_rows(D, r) * 64 + 8 * (size_t)kPairWaves * 64;
+}
+
+// offp[q·NT + t]: LDS offset (doubles) of core entry q's factor in table t
+__global__ void pred_pair_offs_kernel(const int32_t* __restrict__ I0, int Q, int D, int R,
+                                      int32_t* __restrict__ offp) {
+  const int NT = (D + 1) / 2;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= Q * NT) return;
+  const int q = x / NT, t = x - q * NT;
+  const int a = I0[q + Q * (2 * t)];
+  const int row = 2 * t + 1 < D ? t * R * R + a * R + I0[q + Q * (2 * t + 1)]
+                                : t * R * R + a;    // the odd last dimension: r rows
+  offp[x] = row * 64;
+}
+
+template <int NT>
+__global__ __launch_bounds__(64 * kPairWaves) void pred_vphase_pairs_kernel(
+    const double* __restrict__ w, const double* __restrict__ T, const int32_t* __restrict__ offp,
+    int D, int R, long long Ntest, int Q, double* __restrict__ fhat) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* pp = (double*)smem;                                   // [row][64]
+  const int tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);
+  const int s = blockIdx.y;
+  const long long i0 = (long long)blockIdx.x * 64;
+  const long long i = i0 + lane;
+  const bool ok = i < Ntest;
+  const double* Ts = T + (size_t)s * D * R * Ntest + (ok ? i : i0);
+  const int rows = (D / 2) * R * R + (D & 1) * R;
+  double* red = pp + (size_t)rows * 64;
+  // tables: wave w builds tables w, w + 4, ..; the 2·R temp rows of a table (512 contiguous
+  // bytes each) are loaded together, then the R² products go to LDS
+  for (int t = wv; t < NT; t += kPairWaves) {
+    double a[5], b[5];
+    const bool two = 2 * t + 1 < D;
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      a[x] = x < R ? gptr(Ts)[(size_t)((2 * t) * R + x) * Ntest] : 0.0;
+      b[x] = (x < R && two) ? gptr(Ts)[(size_t)((2 * t + 1) * R + x) * Ntest] : 1.0;
+    }
+    double* dst = pp + (size_t)t * R * R * 64 + lane;
+    if (two) {
+#pragma unroll
+      for (int x = 0; x < 5; ++x)
+#pragma unroll
+        for (int y = 0; y < 5; ++y)
+          if (x < R && y < R) dst[(x * R + y) * 64] = a[x] * b[y];
+    } else {
+#pragma unroll
+      for (int x = 0; x < 5; ++x)
+        if (x < R) dst[x * 64] = a[x];
+    }
+  }
+  __syncthreads();
+  const auto* of = cptr(offp);
+  const auto* wq = cptr(w + (size_t)s * Q);
+  const int qa = (Q * wv) / kPairWaves, qb = (Q * (wv + 1)) / kPairWaves;
+  double f0 = 0.0, f1 = 0.0;
+  int q = qa;
+  for (; q + 2 <= qb; q += 2) {
+    double v0 = pp[of[q * NT] + lane], v1 = pp[of[(q + 1) * NT] + lane];
+#pragma unroll
+    for (int t = 1; t < NT; ++t) {
+      v0 *= pp[of[q * NT + t] + lane];
+      v1 *= pp[of[(q + 1) * NT + t] + lane];
+    }
+    f0 = fma(wq[q], v0, f0);
+    f1 = fma(wq[q + 1], v1, f1);
+  }
+  if (q < qb) {
+    double v0 = pp[of[q * NT] + lane];
+#pragma unroll
+    for (int t = 1; t < NT; ++t) v0 *= pp[of[q * NT + t] + lane];
+    f0 = fma(wq[q], v0, f0);
+  }
+  red[wv * 64 + lane] = f0 + f1;
+  __syncthreads();
+  if (wv == 0 && ok) {
+    double f = red[lane];
+#pragma unroll
+    for (int x = 1; x < kPairWaves; ++x) f += red[x * 64 + lane];
+    fhat[(size_t)s * Ntest + i] = f;
+  }
+}
+
 static size_t pred_vphase_lds_bytes(int D, int r, int Q) {
   return al16(8 * (size_t)D * r * 65) + al16(4 * (size_t)Q * D) + al16(8 * (size_t)Q);
 }
@@ -455,16 +551,26 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
   }
   double* T = nullptr;
   const size_t tbytes = (per_sample * chunk + 255) / 256 * 256;
-  hipError_t e = hipMallocAsync((void**)&T, tbytes + 4 * (size_t)Q * D, st);
+  const int NTp = pred_pair_tables(D);
+  hipError_t e = hipMallocAsync((void**)&T, tbytes + 4 * (size_t)Q * D + 4 * (size_t)Q * NTp, st);
   if (e != hipSuccess) return e;
   int32_t* offs = (int32_t*)((char*)T + tbytes);
+  int32_t* offp = offs + (size_t)Q * D;
   hipLaunchKernelGGL(pred_offs_kernel, dim3((Q * D + 255) / 256), dim3(256), 0, st, I0, Q, D, r,
                      offs);
+  hipLaunchKernelGGL(pred_pair_offs_kernel, dim3((Q * NTp + 255) / 256), dim3(256), 0, st, I0, Q,
+                     D, r, offp);
   const size_t rlds = 8 * (size_t)D * r * 64;
-  static const bool tile_vphase = [] {
+  // V-phase variant: "pairs" (default where the tables fit: ⌈D/2⌉ ≤ 8 and ≤ 96 KB), "rows", "tile"
+  const int vmode = [] {
     const char* ev = std::getenv("GPTSGLD_PRED_VPHASE");
-    return ev && std::strcmp(ev, "tile") == 0;
+    if (ev && std::strcmp(ev, "tile") == 0) return 2;
+    if (ev && std::strcmp(ev, "rows") == 0) return 1;
+    return 0;
   }();
+  const size_t plds = pred_pairs_lds_bytes(D, r);
+  const bool pairs = vmode == 0 && r <= 5 && NTp <= 8 && plds <= 96 * 1024;
+  const bool tile_vphase = vmode == 2;
   const size_t vlds = pred_vphase_lds_bytes(D, r, Q);
   for (int s0 = 0; s0 < S && e == hipSuccess; s0 += chunk) {
     const int Sc = std::min(chunk, S - s0);
@@ -474,6 +580,32 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     if (e != hipSuccess) break;
     if (timing) (void)hipEventRecord(ev[1], st);
     dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
+    if (pairs) {
+      switch (NTp) {
+#define PCASE(NN)                                                                              \
+  case NN: {                                                                                   \
+    static std::atomic<uint64_t> attr{0};                                                      \
+    e = set_max_lds_once((const void*)pred_vphase_pairs_kernel<NN>, 160 * 1024, attr);         \
+    if (e != hipSuccess) break;                                                                \
+    hipLaunchKernelGGL(pred_vphase_pairs_kernel<NN>, vg, dim3(64 * kPairWaves), plds, st,      \
+                       w + (size_t)s0 * Q, T, offp, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest);\
+    e = hipGetLastError();                                                                     \
+  } break;
+        PCASE(1) PCASE(2) PCASE(3) PCASE(4) PCASE(5) PCASE(6) PCASE(7) PCASE(8)
+#undef PCASE
+        default: e = hipErrorInvalidValue;
+      }
+      if (timing && e == hipSuccess) {
+        (void)hipEventRecord(ev[2], st);
+        (void)hipEventSynchronize(ev[2]);
+        float a = 0.f, b = 0.f;
+        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+        (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+        timing->gemm_ms += a;
+        timing->vphase_ms += b;
+      }
+      continue;
+    }
     if (!tile_vphase) {
       if (rlds > 64 * 1024) {
         static std::atomic<uint64_t> attr{0};

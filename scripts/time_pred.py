@@ -2,7 +2,7 @@
 
     python scripts/time_pred.py [--S 256] [--n 500] [--r 5] [--Ntest 30000]
 Prints ms per call and the GEMM's fp64 TFLOP/s for each GPTSGLD_PRED_TILE (22, 42, 24, 44) and
-GPTSGLD_PRED_VPHASE (rows, tile) combination asked for.
+GPTSGLD_PRED_VPHASE (pairs, rows, tile) combination asked for.
 """
 import argparse
 import os
@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--Ntest", type=int, default=30000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tiles", default="22,42,24,44")
-    ap.add_argument("--vphases", default="rows", help="GPTSGLD_PRED_VPHASE values to compare (rows, tile)")
+    ap.add_argument("--vphases", default="pairs,rows",
+                    help="GPTSGLD_PRED_VPHASE values to compare (pairs, rows, tile)")
     a = ap.parse_args()
     import torch
     from gpt_amd import GPT_SGLD as G
