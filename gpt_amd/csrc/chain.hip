@@ -155,7 +155,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   double* X = (double*)(smem + L::o_un) + k * L::x_dbl;         // this wave's scratch
   double* xi_l = X;                                             // noise slots (before expm)
   double* pw0 = pbuf + k * (kChainBufs * G * 64 * J);           // this wave's staged rows
-  double* bscr = wVr + G * kChainQS + k * G * R * kChainRunS;   // per row
+  [[maybe_unused]] double* bscr = wVr + G * kChainQS + k * G * R * kChainRunS;   // per row
 
   // steps t0 .. tend-1 of this chain in one launch (a chunk of at most one epoch): U^(k) stays in
   // registers and w in LDS between steps; the next batch's rows and targets are fetched during
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     // (b) temp[k,l,row] and 1/temp for the G rows: R partial dots per lane, reduced through this
     // wave's LDS scratch by 8-lane groups (lane 8l+s sums 8 partials of output l, DPP finishes)
     double* tsl = temp_l + slot * L::TS;
-    const int rl = min(ln >> 3, R - 1), rs = ln & 7;
+    const int rl = min(ln >> 3, R - 1);
 #if CHAIN_BFLY
     {
       // the G·R partial dots of this lane, reduced over the wave by one register butterfly
@@ -362,6 +362,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       }
     }
 #else
+    const int rs = ln & 7;
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) {
       double v[R];

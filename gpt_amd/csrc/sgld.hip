@@ -24,6 +24,11 @@ namespace gpt {
           (long long)__builtin_amdgcn_s_memtime();                                         \
   } while (0)
 
+#ifndef GPT_TOUCH
+#define GPT_TOUCH 1       // L2 touch of the next batch's rows during the V-phase
+#endif
+constexpr int kTouch = 4;   // row pairs per wave: 2·kNW·kTouch = 64 rows >= the minibatch
+
 template <int R>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) void sgld_step_kernel(StepParams P,
                                                         const ChainDesc* __restrict__ chains,
@@ -61,6 +66,23 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   const int Bt = min(m, P.N - start);
   const int32_t* ord = C.order + (size_t)(e & 1) * P.N + start;
   const bool wblock = (k == D);
+  const long long t1 = t + 1;
+  const int e1 = (int)(t1 / P.nb), b1 = (int)(t1 - (long long)e1 * P.nb);
+  const int s1 = b1 * m;
+  const bool has_next = t1 < P.total_steps;
+  const int B1 = has_next ? min(m, P.N - s1) : 0;
+  const int32_t* ord1 = C.order + (size_t)((has_next ? e1 : e) & 1) * P.N + (has_next ? s1 : start);
+  // rows of the next batch this lane touches into L2 during the V-phase (P5 streams them at the
+  // end of the step): lanes 0-31 / 32-63 of wave w cover rows 2(w + kNW·x) + {0, 1}
+  int trow[kTouch];
+  const bool touch = GPT_TOUCH && k < D && has_next;
+  if (touch) {
+#pragma unroll
+    for (int x = 0; x < kTouch; ++x) {
+      const int i = 2 * (wv + kNW * x) + ((tid & 63) >> 5);
+      trow[x] = gptr(ord1)[min(i, B1 - 1)];      // past the batch: its last row again
+    }
+  }
   STAMP(0);
 
   // ---- P0: stage temp (this batch), I, w, batch rows and targets
@@ -86,13 +108,18 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   STAMP(1);
 
   const long long koff = (long long)n * k, rstride = (long long)n * D;
-  const long long t1 = t + 1;
-  const int e1 = (int)(t1 / P.nb), b1 = (int)(t1 - (long long)e1 * P.nb);
-  const int s1 = b1 * m;
-  const bool has_next = t1 < P.total_steps;
-  const int B1 = has_next ? min(m, P.N - s1) : 0;
-  const int32_t* ord1 = C.order + (size_t)((has_next ? e1 : e) & 1) * P.N + (has_next ? s1 : start);
-
+  // one 4-B load per 128-B line of the rows: the lines reach this XCD's L2 while the V-phase below
+  // works from LDS only; the loaded words are consumed (an empty asm) only after the V-phase, so
+  // their wait sits at its end (checked in the ISA: an LDS-DMA touch instead puts a vmcnt wait in
+  // front of the V-phase's LDS reads, and so did batching P0's loads ahead of it)
+  int tv[kTouch];
+  if (touch) {
+    const unsigned o = min(32u * (unsigned)(tid & 31), 2u * n - 1u);   // in 4-B words
+#pragma unroll
+    for (int x = 0; x < kTouch; ++x)
+      tv[x] = gptr((const int*)(C.phi + koff + (long long)trow[x] * rstride))[o];
+    asm volatile("" ::: "memory");
+  }
   // ---- P1: V, fhat, residual, A[:,k,:] (GPT_SGLD.jl:384-399)
   {
     auto vout = [&](int comp, int i, double v) {
@@ -103,6 +130,10 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       vphase_tile<R, VCfg<R>::ICV_SMALL>(temp_l, MP, IT_l, w_l, Q, D, k >= D ? 0 : k, Bt, vout);
     else
       vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, IT_l, w_l, Q, D, k >= D ? 0 : k, Bt, vout);
+  }
+  if (touch) {
+#pragma unroll
+    for (int x = 0; x < kTouch; ++x) asm volatile("" ::"v"(tv[x]));
   }
   __syncthreads();
   STAMP(2);
