@@ -1,6 +1,6 @@
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
-for v in nt base; do
+for v in ${VARIANTS:-nt base}; do
   lib=gpt_amd/libgptsgld_$v.so; [ "$v" = base ] && lib=gpt_amd/libgptsgld.so
   echo "=== $v"
   GPTSGLD_LIB=$lib timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "grid or rmsprop or classif or wonly or gpnt" > gpurun_out/gt_$v.log 2>&1 || { echo "tests $v failed"; tail -15 gpurun_out/gt_$v.log; exit 1; }
