@@ -143,6 +143,28 @@ def test_pred_stacked_samples_mfma(n, D, Nt, r, Q, S):
     assert rel(f1, f[S - 1]) < 1e-12
 
 
+@pytest.mark.parametrize("D", [3, 8])
+def test_pred_vphase_pairs_equals_rows(D, monkeypatch):
+    """The pair-table V-phase (default, r <= 5) and the lanes-as-rows V-phase
+    (GPTSGLD_PRED_VPHASE=rows) give the same predictions up to the association of the D factors."""
+    n, Nt, r, Q, S = 64, 777, 5, 60, 6
+    rng = np.random.default_rng(D)
+    X = rng.standard_normal((Nt, D)); Z = rng.standard_normal((n, D)); b = 2 * np.pi * rng.random((n, D))
+    phi = R.feature(X, 1.0 + 0.1 * rng.random(D), 1.0, math.sqrt(n / Q ** (1.0 / D)), Z, b)
+    I = R.samplenz(r, D, Q, 7)
+    ws = rng.standard_normal((Q, S))
+    Us = np.stack([R.init_state(n, r, D, Q, 70 + s)[1] for s in range(S)], axis=3)
+    yt = rng.standard_normal(Nt)
+    Uf = Us.reshape((n, r, D * S), order="F")
+    mean_p, _ = G().pred_mean(ws, Uf, I, phi, yt)
+    monkeypatch.setenv("GPTSGLD_PRED_VPHASE", "rows")
+    mean_r, _ = G().pred_mean(ws, Uf, I, phi, yt)
+    monkeypatch.delenv("GPTSGLD_PRED_VPHASE")
+    assert rel(mean_p, mean_r) < 1e-13
+    f = np.stack([R.pred(ws[:, s], Us[..., s], I, phi) for s in range(S)])
+    assert rel(mean_p, f.mean(axis=0)) < 1e-12
+
+
 # ----------------------------------------------------------------------------- sampler
 CASES = {
     # name: (n, D, N, r, Q, m, burnin, maxepoch, store_every, langevin, stiefel)
