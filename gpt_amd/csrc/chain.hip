@@ -268,11 +268,11 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 
   constexpr int TPW = (J >= 8 && WV > 4) ? 1 : kChainTasks;   // one task per wave at J = 8, D > 4
   for (;;) {                             // ---------------------------------- one SGLD step
-  // thread ids the compiler cannot see through: per-lane addresses are formed inside the step
-  // instead of being hoisted out of the step loop and held in registers across it
-  int tid_o = threadIdx.x;
-  asm volatile("" : "+v"(tid_o));
-  const int tid = tid_o, lane = tid_o & 63;
+  // thread ids formed inside the step from v_mbcnt (not threadIdx.x): per-lane addresses are not
+  // hoisted out of the step loop, and v0 need not be kept — the register-bound kernel used to spill
+  // it and reload it (and values derived from it) in the Stiefel phase, each reload a vmcnt(0)
+  // wait behind the next batch's row DMA (−4 % step time)
+  const int lane = lane_id(), tid = 64 * k + lane;
   for (int o = tid; o < G; o += NTH) wVr[o * kChainQS + kChainQP] = 0.0;   // gather zero slots
   // (re-derived every step rather than held across the Stiefel phase, where registers are short)
   // this wave's V-task temp indices (< 256, four per register), fixed for the step

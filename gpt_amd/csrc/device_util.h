@@ -14,6 +14,15 @@ __device__ __forceinline__ T* uni_ptr(T* p) {
   return (T*)(((unsigned long long)hi << 32) | lo);
 }
 
+// Lane id (0..63) from v_mbcnt, formed where it is used: nothing has to keep threadIdx.x (v0)
+// alive, which long kernels would otherwise spill to scratch and reload — each reload a vmcnt(0)
+// wait behind every load still in flight.
+__device__ __forceinline__ int lane_id() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // Order LDS traffic between the lanes of ONE wave (no workgroup barrier).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -506,7 +515,7 @@ __device__ __forceinline__ void wave_solve_body(double* M, double* X, long long*
 template <int NV>
 __device__ __forceinline__ void wave_sum_to_lds(double (&v)[NV], double* dst) {
   constexpr int NB = NV <= 8 ? 8 : (NV <= 16 ? 16 : (NV <= 32 ? 32 : 64));
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
   double b[NB];
 #pragma unroll
   for (int x = 0; x < NB; ++x) b[x] = x < NV ? v[x] : 0.0;
@@ -518,7 +527,7 @@ __device__ __forceinline__ void wave_sum_to_lds(double (&v)[NV], double* dst) {
 template <int NV>
 __device__ __forceinline__ void wave_sum_to_lds(double (&v)[2 * NV], double* dst, double* dst2) {
   constexpr int NB = 2 * NV <= 8 ? 8 : (2 * NV <= 16 ? 16 : (2 * NV <= 32 ? 32 : 64));
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_id();
   double b[NB];
 #pragma unroll
   for (int x = 0; x < NB; ++x) b[x] = x < 2 * NV ? v[x] : 0.0;
