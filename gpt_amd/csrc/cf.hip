@@ -92,6 +92,11 @@ __device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int w
   cf_gram(M, G, rows, R, Mg);
   __syncthreads();
   for (int row = tid; row < rows; row += kCfNT) {
+    // an offset the compiler cannot see through: the R² Gram entries are read from LDS per row
+    // rather than hoisted out of the row loop into registers (at r = 20 that spilled thousands
+    // of values)
+    int zo = 0;
+    asm volatile("" : "+v"(zo));
     double x[R], u[R];
 #pragma unroll
     for (int l = 0; l < R; ++l) {
@@ -102,7 +107,7 @@ __device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int w
     for (int bb = 0; bb < R; ++bb) {
       double s = 0.0;
 #pragma unroll
-      for (int a2 = 0; a2 < R; ++a2) s = fma(u[a2], Mg[a2 * R + bb] + Mg[bb * R + a2], s);
+      for (int a2 = 0; a2 < R; ++a2) s = fma(u[a2], Mg[zo + a2 * R + bb] + Mg[zo + bb * R + a2], s);
       gptr_w(G)[row + (size_t)rows * bb] = x[bb] - s / 2;
     }
   }
@@ -140,6 +145,8 @@ __device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int w
   }
   __syncthreads();
   for (int row = tid; row < rows; row += kCfNT) {
+    int zo = 0;                       // F read from LDS per row (see the proj loop)
+    asm volatile("" : "+v"(zo));
     double x[NN];
 #pragma unroll
     for (int l = 0; l < R; ++l) {
@@ -150,7 +157,7 @@ __device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int w
     for (int l = 0; l < R; ++l) {
       double s = 0.0;
 #pragma unroll
-      for (int a2 = 0; a2 < NN; ++a2) s = fma(x[a2], F[a2 * R + l], s);
+      for (int a2 = 0; a2 < NN; ++a2) s = fma(x[a2], F[zo + a2 * R + l], s);
       gptr_w(M)[row + (size_t)rows * l] = s;
       gptr_w(G)[row + (size_t)rows * l] = 0.0;
     }

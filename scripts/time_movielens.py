@@ -1,5 +1,5 @@
 """Wall-clock of the MovieLens-100k CF samplers on the GPU (config 5): the live GPT_fullw_sideinfo
-run of 100k_movielensExperiment.jl:723-730 (fold 1, r = 15, m = 100) and one GPT_fullw_gibbs
+run of 100k_movielensExperiment.jl:723-730 (fold 1, r = 15 or --r, m = 100) and one GPT_fullw_gibbs
 sweep, printed as one JSON line.  Usage: python scripts/time_movielens.py [--epochs E]"""
 import argparse
 import json
@@ -16,11 +16,12 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=5)
+    ap.add_argument("--r", type=int, default=15, help="rank (BASELINE config 5 is r = 20)")
     args = ap.parse_args()
     from gpt_amd import movielens
     d = np.load(os.path.join(ROOT, "tests", "golden", "ml100k.npz"))
     tr, te, ud, md, mu, sd = movielens.fold(d, 1)
-    w0 = np.random.default_rng(17).standard_normal((15, 15))
+    w0 = np.random.default_rng(17).standard_normal((args.r, args.r))
     movielens.GPT_fullw_sideinfo(tr, ud, md, te, 0.8, 0.1, 1.0, w0, 100, 1e-4, 1e-6, 0.5, 0.25,
                                  0.5, 0, 1, 17, mu, sd)                        # warm-up / load
     t = time.perf_counter()
@@ -41,7 +42,7 @@ def main():
     o5 = movielens.GPT_fullw_sideinfo_folds([f[0] for f in fl], ud, md, [f[1] for f in fl], *args5,
                                             [f[4] for f in fl], [f[5] for f in fl])
     t_fold = (time.perf_counter() - t) / args.epochs
-    print(json.dumps({"workload": "ml-100k fold 1, r=15", "sideinfo_sgd_s_per_epoch": ts,
+    print(json.dumps({"workload": "ml-100k fold 1, r=%d" % args.r, "sideinfo_sgd_s_per_epoch": ts,
                       "sideinfo_steps_per_s": 800 / ts, "sideinfo_testRMSE": list(out[5]),
                       "gibbs_s_per_sweep": tg, "gibbs_testRMSE": list(g[5]),
                       "five_folds_separate_s_per_epoch": t_sep,
