@@ -125,7 +125,7 @@ __device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int w
       X0[o] = tt * v;
     }
     wave_sync();
-    if (wave_expm<NN>(X0) && tid == 0) flag[0] = 1;
+    if (wave_expm<NN, false>(X0) && tid == 0) flag[0] = 1;   // 1024-thread block: LDS GEPP
   } else if (wv == 1) {
     const int ln = tid & 63;
     for (int o = ln; o < R * R; o += 64) X1[o] = -tt * Ag[o];

@@ -604,11 +604,82 @@ __device__ __forceinline__ bool wave_solve_dd(const double* M, double* X) {
   return true;
 }
 
+// wave_solve_dd for 32 < NN <= 64, where [M | X] has more columns than the wave has lanes: the
+// factorisation and the right-hand sides go in two passes of one column per lane, with the
+// factors kept in LDS between them (F, NN² doubles: multipliers below the diagonal, U above it,
+// the Newton-refined pivot reciprocals on it).  Every column sees exactly the operations of
+// wave_solve_dd (the pivot lane's multipliers are the doubles the other lanes would form).
+template <int NN>
+__device__ __noinline__ bool wave_solve_dd2(const double* Mg, double* Xg, double* Fg) {
+  static_assert(NN > 32 && NN <= 64, "two-pass register LU");
+  typedef __attribute__((address_space(3))) double lds_d;   // LDS arguments: ds_*, not flat_*
+  const lds_d* M = (const lds_d*)Mg;
+  lds_d* X = (lds_d*)Xg;
+  lds_d* F = (lds_d*)Fg;
+  const int lane = lane_id();
+  bool dd = true;
+  if (lane < NN) {
+    double off = 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+      if (i != lane) off += fabs(M[i * NN + lane]);
+    dd = fabs(M[lane * NN + lane]) > off;
+  }
+  if (!__all(dd)) return false;
+  double col[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) col[i] = M[i * NN + (lane < NN ? lane : 0)];
+#pragma unroll
+  for (int p = 0; p < NN; ++p) {              // getrf: the pivot lane writes its multipliers
+    if (lane == p) {
+      const double rp = rcp_nr(col[p]);
+      F[p * NN + p] = rp;
+#pragma unroll
+      for (int i = p + 1; i < NN; ++i) F[i * NN + p] = col[i] * rp;
+    }
+    wave_sync();
+#pragma unroll
+    for (int i = p + 1; i < NN; ++i) col[i] -= F[i * NN + p] * col[p];
+  }
+#pragma unroll
+  for (int i = 0; i < NN - 1; ++i)            // U above the diagonal: column k from lane k
+    if (i < lane && lane < NN) F[i * NN + lane] = col[i];
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < NN; ++i) col[i] = X[i * NN + (lane < NN ? lane : 0)];
+  // Each step's factor reads hang off an offset that depends on the previous step's result: the
+  // scheduler cannot issue all NN² reads up front (which spilled ~1 200 values at 256 VGPRs).
+#pragma unroll
+  for (int p = 0; p < NN; ++p) {              // L solve
+    int zo = 0;
+    asm volatile("" : "+v"(zo) : "v"(col[p]));
+#pragma unroll
+    for (int i = p + 1; i < NN; ++i) col[i] -= F[zo + i * NN + p] * col[p];
+  }
+#pragma unroll
+  for (int k = NN - 1; k >= 0; --k) {         // back substitution
+    int zo = 0;
+    asm volatile("" : "+v"(zo) : "v"(col[k]));
+    col[k] = col[k] * F[zo + k * NN + k];
+#pragma unroll
+    for (int i = 0; i < k; ++i) col[i] -= col[k] * F[zo + i * NN + k];
+  }
+  wave_sync();
+  if (lane < NN) {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) X[i * NN + lane] = col[i];
+  }
+  wave_sync();
+  return true;
+}
+
 // expm(A) for an NN×NN matrix held in S[0..NN²) (row-major; overwritten).  Padé
 // scaling-and-squaring of Julia Base 0.3 expm! (Higham 2005; thresholds 0.015/0.25/0.95/2.1,
 // 13th order above, θ13 = 5.4).  Scratch S: 7 NN² doubles; the result is left at S + NN².
 // Returns true if the result contains a NaN (the geod bail-out of GPT_SGLD.jl:23-26).
-template <int NN>
+// kRegLU2 = false keeps the LDS GEPP for 32 < NN <= 64 (callers at a 128-VGPR budget, where the
+// two-pass register LU spills).
+template <int NN, bool kRegLU2 = true>
 __device__ bool wave_expm(double* S, long long* st = nullptr) {
   const int lane = threadIdx.x & 63;
   // diagnostic stamps (slots 11-14 of the caller's stamp row; grid engine stamp builds only)
@@ -704,6 +775,7 @@ __device__ bool wave_expm(double* S, long long* st = nullptr) {
   wave_sync();
   bool solved = false;
   if constexpr (2 * NN <= 64) solved = wave_solve_dd<NN>(M, X);
+  else if constexpr (kRegLU2 && NN <= 64) solved = wave_solve_dd2<NN>(M, X, U);   // U, V dead here
   if (!solved) wave_solve<NN>(M, X, st);
   GPT_XST(13);
   for (int z = 0; z < si; ++z) {
