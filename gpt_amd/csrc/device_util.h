@@ -420,7 +420,9 @@ template <int NN>
 __device__ __forceinline__ void wave_solve_body(double* M, double* X, long long* st);
 template <int NN>
 __device__ __noinline__ void wave_solve_ool(double* M, double* X, long long* st) {
-  wave_solve_body<NN>(M, X, st);
+  __builtin_assume(__builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)M));
+  __builtin_assume(__builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)X));
+  wave_solve_body<NN>(M, X, st);               // M, X are LDS (see wave_expm): ds_*, not flat_*
 }
 template <int NN>
 __device__ __forceinline__ void wave_solve(double* M, double* X, long long* st = nullptr) {
@@ -681,6 +683,10 @@ __device__ __noinline__ bool wave_solve_dd2(const double* Mg, double* Xg, double
 // two-pass register LU spills).
 template <int NN, bool kRegLU2 = true>
 __device__ bool wave_expm(double* S, long long* st = nullptr) {
+  // S is LDS (every caller's expm scratch): said so, the compiler infers the local address space
+  // for everything derived from it and emits ds_* instead of flat_* (this function is compiled
+  // out of line, where the caller's address space is not visible)
+  __builtin_assume(__builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)S));
   const int lane = threadIdx.x & 63;
   // diagnostic stamps (slots 11-14 of the caller's stamp row; grid engine stamp builds only)
 #define GPT_XST(i)                                                        \
