@@ -535,6 +535,9 @@ static int session_graph(gpt_sgld_session* s, int len, hipGraphExec_t* out) {
   ee = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
   if (ee != hipSuccess) { (void)hipGraphDestroy(g); return hip_fail(ee, "hipGraphInstantiate"); }
   s->graphs.push_back({b0, len, g, x});
+  // upload now (ordered on the session stream), so a graph prepared ahead of a timed region does
+  // not pay its first-launch upload inside it
+  HIPCHK(hipGraphUpload(x, s->stream));
   *out = x;
   return GPT_OK;
 }
