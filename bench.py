@@ -5,8 +5,9 @@
 
 Workload (BASELINE config 3/4): kin40k — Ntrain = 10 000 rows (the reference's
 own kin40k_train files, whitened as kin40kExperiment.jl:25-37), D = 8, n = 500 random
-features per dimension, rank r = 5, Q = 200, minibatch m = 50, εw = 1e-4, εU = 1e-7,
-σ² = 0.0476, ℓ/σ_RBF of kin40kExperiment.jl:22-23.  phi (320 MB) is built on the device by
+features per dimension, rank r = 5, Q = 200, minibatch m = 50, σ² = 0.0476, ℓ/σ_RBF of
+kin40kExperiment.jl:22-23, εw = 1e-5, εU = 1e-8 (the script's 1e-4 / 1e-7 diverge at n = 500,
+r = 5 in the oracle and on the GPU alike).  phi (320 MB) is built on the device by
 the feature kernel and stays resident in HBM.  Each GPU runs C independent posterior chains
 (seeds differ, phi shared — BASELINE config 4 has one chain per GPU; C chains per GPU is the
 same thing with the GPU filled).  A "step" is one SGLD step of one chain over one minibatch;
@@ -128,6 +129,17 @@ def cpu_baseline(phi_np, y_np, I, args, seconds):
                                    T, sT, T, dtT))
 
 
+def chain_seeds(rank, C):
+    """param_seed of chain c on this rank: rank·C + c + 1 — distinct over all ranks and chains
+    (kin40kExperiment.jl:68 seeds its chains 1..J)."""
+    return [rank * C + c + 1 for c in range(C)]
+
+
+def scratch_seeds(rank, C):
+    """Seeds of the clock warm-up's scratch chains (disjoint from chain_seeds at any world size)."""
+    return [(1 << 40) + rank * C + c for c in range(C)]
+
+
 def launch_command(argv, nproc, port, script=None):
     """The torchrun command bench.py re-runs itself under for --gpus N > 1 (one rank per GPU)."""
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
@@ -157,6 +169,79 @@ def max_over_ranks(dt, device=None):
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def compose_line(v):
+    """The bench's JSON line (rank 0) from the measured values in namespace v.  Every N keeps the
+    same fields: cpu_baseline (rank 0's host cores), kernel_us per rank, the single-chain pass."""
+    a = v.args
+    pred_tfs = v.pred_flop / (v.pred_ms * 1e-3) / 1e12
+    gemm_tfs = v.pred_flop / (v.gemm_ms * 1e-3) / 1e12
+    return {
+        "metric": ("SGLD steps/sec (kin40k, n_feat=500/dim, r=5)" if a.workload == "kin40k"
+                   else "SGLD steps/sec (PowerPlant, n_feat=500/dim, r=5, minibatch 256)"),
+        "value": v.value,
+        "unit": "chain-steps/s",
+        "n_gpus": v.world,
+        "world_size_seen": v.world_seen,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "clock_warm_ms": v.warm_ms,
+        "ms_per_step": v.ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": ("%s reference files (tests/golden/%s.npz), whitened; features on device"
+                 % (a.workload, a.workload)),
+        "config": {"workload": v.wdesc, "Ntrain": v.N, "Ntest": v.Nte,
+                   "D": v.D, "n_features": v.n, "r": v.r, "Q": v.Q, "minibatch": v.m,
+                   "chains_per_gpu": v.C, "epsw": a.epsw, "epsU": a.epsU,
+                   "signal_var": a.signal_var, "parallelism": "chains%dx%d" % (v.C, v.world),
+                   "engine": v.info["engine"], "workgroups_per_launch": v.info["workgroups"],
+                   "threads_per_workgroup": v.info["threads"], "lds_bytes": v.info["lds_bytes"]},
+        "roofline": {"bound": "hbm", "achieved": v.achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": v.achieved / HBM_PEAK_GBS, "traffic": v.traffic,
+                     "traffic_source": v.traffic_src,
+                     "kernel": ("chain_kernel<%d,J,2>" if v.info["engine"] == "chain"
+                                else "sgld_step_kernel<%d>") % v.r, "kernel_us": v.k_us,
+                     "kernel_us_per_rank": v.k_us_ranks,
+                     "kernel_us_note": "per step of all chains; the chain engine runs up to "
+                                       "one epoch of steps per launch (one event pair per "
+                                       "launch, total / steps)",
+                     "algorithmic_bytes_per_launch": v.bytes_launch,
+                     "algorithmic_bytes_per_step": v.bytes_launch,
+                     "steps_run_per_chain": v.steps_run},
+        "cpu_baseline": v.cpu,
+        "test_rmse": v.quality["test_rmse"],
+        "test_rmse_note": v.quality["note"],
+        "quality": v.quality,
+        "allreduce_ms": v.allreduce_ms,
+        "pred": {"samples": v.npred, "Ntest": v.Nte, "ms": v.pred_ms, "gemm_flop": v.pred_flop,
+                 "achieved_tflops": pred_tfs, "peak_tflops": FP64_MFMA_PEAK_TFS,
+                 "frac": pred_tfs / FP64_MFMA_PEAK_TFS,
+                 "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + pred_vphase_pairs_kernel",
+                 "note": "whole stacked-sample call timed with events (GEMM + V-phase)",
+                 "gemm_ms": v.gemm_ms, "vphase_ms": v.vphase_ms,
+                 "gemm_roofline": {"bound": "mfma", "achieved": gemm_tfs,
+                                   "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                   "frac": gemm_tfs / FP64_MFMA_PEAK_TFS},
+                 "final_state_ensemble_rmse": v.rmse_final},
+        "single_chain": v.single,
+        "single_chain_steps_per_s": v.single["steps_per_s"] if v.single else None,
+    }
+
+
+def gather_over_ranks(x, device=None):
+    """[x of rank 0, .., x of rank N-1] (every rank gets the list)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return [x]
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
 
 
 def main():
@@ -256,37 +341,39 @@ def main():
     epochs = -(-need // nb) + 1
     epochs_total = max(args.epochs, epochs)
     last = max(1, min(args.last_epochs, epochs_total))
-    seeds = [1000 * rank + c + 1 for c in range(C)]
+    seeds = chain_seeds(rank, C)
     # burn-in = all but the last `last` epochs: the timed steps store nothing, the epoch-end
     # samples of the last epochs feed the converged posterior mean
     sess = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var,
                        epochs_total - last, last, seeds, store_every=nb, store=True,
                        engine=args.engine)
     info = sess.info()
+    sess.run(args.warmup)
+    sess.prepare(args.steps)           # capture the timed steps' graphs outside the timed region
+    sess.sync()
     warm_ms = 0.0
     warm_steps = 0                     # chain steps of the scratch session (profile accounting)
+    sw = None
     if args.clock_warm_ms > 0:
-        # bring the GPU to its sustained clock before the timed region (a fresh box idles at low
-        # clocks; the driver's --warmup 5 is ~1 ms of work): a scratch session of the same shape
-        # and chain count, discarded — the timed chains' state is untouched
+        # Bring the GPU to its sustained clock right before the timed region.  The chain kernel's
+        # cycles per step are fixed (≈216 k); its time per step follows the shader clock, which
+        # drops during any idle gap of a millisecond or more (host work, frees) and takes
+        # milliseconds to ramp back (scripts/timeline.py: 2.09 GHz after a gap, 2.33-2.39 GHz
+        # under sustained load).  The driver's 20 timed steps are ~2 ms, so without this they
+        # would measure the ramp.  A scratch session of the same shape and chain count runs the
+        # same work (the timed chains' state is untouched) and stays allocated until the timed
+        # region is over, so no free (a device synchronisation) sits between it and the timing.
+        ep_warm = 2 + int(args.clock_warm_ms / 15.0)
         sw = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0,
-                         2, [10 ** 6 + c for c in range(C)], store=False, engine=args.engine)
+                         ep_warm, scratch_seeds(rank, C), store=False, engine=args.engine)
         tw = time.perf_counter()
-        while (time.perf_counter() - tw) * 1000.0 < args.clock_warm_ms:
-            if sw.steps_done >= sw.total_steps:
-                sw.close()
-                sw = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var,
-                                 0, 2, [10 ** 6 + c for c in range(C)], store=False,
-                                 engine=args.engine)
+        while ((time.perf_counter() - tw) * 1000.0 < args.clock_warm_ms
+               and sw.steps_done < sw.total_steps):
             ns = min(nb, sw.total_steps - sw.steps_done)
             sw.run(ns)
             sw.sync()
             warm_steps += ns
         warm_ms = (time.perf_counter() - tw) * 1000.0
-        sw.close()
-    sess.run(args.warmup)
-    sess.prepare(args.steps)           # capture the timed steps' graphs outside the timed region
-    sess.sync()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -301,9 +388,13 @@ def main():
     value = total_steps / dt
     ms_per_step = 1000.0 * dt / args.steps
 
-    # per-launch kernel time (hipEvents around each step-kernel launch on the session stream)
+    # per-launch kernel time (hipEvents around each step-kernel launch on the session stream),
+    # right behind the timed steps at the same clock (before the scratch session's free)
     k_us = sess.time_steps(args.kernel_steps)
     sess.sync()
+    if sw is not None:
+        sw.close()
+    k_us_ranks = gather_over_ranks(k_us, dev)
     bad = [c for c in range(C) if sess.status(c) != 0]
     if bad:
         raise SystemExit("chains %s hit the geodesic NaN bail-out: the timed steps were no-ops" % bad)
@@ -401,64 +492,22 @@ def main():
         s1.close()
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:          # host cores of rank 0's box, any N
         phi_np = np.asfortranarray(phi_tr.cpu().numpy().transpose(2, 1, 0))
         cpu = cpu_baseline(phi_np, ytr, I, args, args.cpu_seconds)
 
     if rank == 0:
-        out = {
-            "metric": ("SGLD steps/sec (kin40k, n_feat=500/dim, r=5)" if args.workload == "kin40k"
-                       else "SGLD steps/sec (PowerPlant, n_feat=500/dim, r=5, minibatch 256)"),
-            "value": value,
-            "unit": "chain-steps/s",
-            "n_gpus": world,
-            "world_size_seen": (dist.get_world_size() if world > 1 else 1),
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "clock_warm_ms": warm_ms,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": ("%s reference files (tests/golden/%s.npz), whitened; features on device"
-                     % (args.workload, args.workload)),
-            "config": {"workload": wdesc, "Ntrain": N, "Ntest": Nte,
-                       "D": D, "n_features": n, "r": r, "Q": Q, "minibatch": m,
-                       "chains_per_gpu": C, "epsw": args.epsw, "epsU": args.epsU,
-                       "signal_var": args.signal_var, "parallelism": "chains%dx%d" % (C, world),
-                       "engine": info["engine"], "workgroups_per_launch": info["workgroups"],
-                       "threads_per_workgroup": info["threads"], "lds_bytes": info["lds_bytes"]},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel": ("chain_kernel<%d,J,2>" if info["engine"] == "chain"
-                                    else "sgld_step_kernel<%d>") % r, "kernel_us": k_us,
-                         "kernel_us_note": "per step of all chains; the chain engine runs up to "
-                                           "one epoch of steps per launch (one event pair per "
-                                           "launch, total / steps)",
-                         "algorithmic_bytes_per_launch": bytes_launch,
-                         "algorithmic_bytes_per_step": bytes_launch,
-                         "steps_run_per_chain": sess.total_steps + warm_steps},
-            "cpu_baseline": cpu,
-            "test_rmse": quality["test_rmse"],
-            "test_rmse_note": quality["note"],
-            "quality": quality,
-            "allreduce_ms": allreduce_ms,
-            "pred": {"samples": npred, "Ntest": Nte, "ms": pred_ms, "gemm_flop": pred_flop,
-                     "achieved_tflops": pred_flop / (pred_ms * 1e-3) / 1e12,
-                     "peak_tflops": FP64_MFMA_PEAK_TFS,
-                     "frac": pred_flop / (pred_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS,
-                     "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + pred_vphase_pairs_kernel",
-                     "note": "whole stacked-sample call timed with events (GEMM + V-phase)",
-                     "gemm_ms": gemm_ms, "vphase_ms": vphase_ms,
-                     "gemm_roofline": {"bound": "mfma", "achieved": pred_flop / (gemm_ms * 1e-3) / 1e12,
-                                       "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                                       "frac": pred_flop / (gemm_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS},
-                     "final_state_ensemble_rmse": rmse_final},
-            "single_chain": single,
-            "single_chain_steps_per_s": single["steps_per_s"] if single else None,
-        }
+        import types
+        world_seen = dist.get_world_size() if world > 1 else 1
+        steps_run = sess.total_steps + warm_steps
+        out = compose_line(types.SimpleNamespace(
+            args=args, value=value, world=world, world_seen=world_seen, warm_ms=warm_ms,
+            ms_per_step=ms_per_step, wdesc=wdesc, N=N, Nte=Nte, D=D, n=n, r=r, Q=Q, m=m, C=C,
+            info=info, achieved=achieved, traffic=traffic, traffic_src=traffic_src, k_us=k_us,
+            k_us_ranks=k_us_ranks, bytes_launch=bytes_launch, steps_run=steps_run, cpu=cpu,
+            quality=quality, allreduce_ms=allreduce_ms, npred=npred, pred_ms=pred_ms,
+            pred_flop=pred_flop, gemm_ms=gemm_ms, vphase_ms=vphase_ms, rmse_final=rmse_final,
+            single=single))
         print(json.dumps(out))
     sess.close()
     if world > 1:

@@ -476,6 +476,17 @@ extern "C" int gpt_sgld_session_set_hyper(gpt_sgld_session* s, int32_t chain, do
   return GPT_OK;
 }
 
+// Destroy every captured graph (after the stream has drained: a launched graph may still run).
+static void session_drop_graphs(gpt_sgld_session* s) {
+  if (s->graphs.empty()) return;
+  (void)hipStreamSynchronize(s->stream);
+  for (auto& g : s->graphs) {
+    (void)hipGraphExecDestroy(g.x);
+    (void)hipGraphDestroy(g.g);
+  }
+  s->graphs.clear();
+}
+
 // Per-chain zeroed gw (Q) | gU (n·r·D) | res (m) buffers of the RMSprop and classification steps.
 static int session_alloc_aux(gpt_sgld_session* s) {
   const StepParams& P = s->P;
@@ -512,6 +523,9 @@ extern "C" int gpt_sgld_session_set_rmsprop(gpt_sgld_session* s, double epsilon,
   const int rc = session_alloc_aux(s);     // moving averages start at 0 (:1143-1144)
   if (rc != GPT_OK) return rc;
   s->P.rms = 1; s->P.rms_eps = epsilon; s->P.rms_alpha = alpha;
+  // graphs prepared before this call (gpt_sgld_session_prepare) captured plain SGLD steps: drop
+  // them so the next run captures RMSprop steps
+  session_drop_graphs(s);
   return GPT_OK;
 }
 
@@ -521,6 +535,7 @@ static int session_graph(gpt_sgld_session* s, int len, hipGraphExec_t* out) {
   for (auto& g : s->graphs)
     if (g.b0 == b0 && g.len == len) { *out = g.x; return GPT_OK; }
   if (s->graphs.size() >= 16) {                // bounded cache: drop the oldest
+    HIPCHK(hipStreamSynchronize(s->stream));   // it may still be running (launches are async)
     (void)hipGraphExecDestroy(s->graphs.front().x);
     (void)hipGraphDestroy(s->graphs.front().g);
     s->graphs.erase(s->graphs.begin());
@@ -607,7 +622,12 @@ extern "C" int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, 
     const int rc = session_prime(s);
     if (rc != GPT_OK) return rc;
   }
-  std::vector<hipEvent_t> ev(2 * cnt, nullptr);
+  struct Events {                          // destroyed on every exit path
+    std::vector<hipEvent_t> v;
+    ~Events() { for (auto e : v) if (e) (void)hipEventDestroy(e); }
+  } evs;
+  evs.v.assign(2 * cnt, nullptr);
+  std::vector<hipEvent_t>& ev = evs.v;
   for (auto& e : ev) HIPCHK(hipEventCreate(&e));
   int rc = GPT_OK;
   s->ran = true;
@@ -634,7 +654,6 @@ extern "C" int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, 
     HIPCHK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
     tot += ms;
   }
-  for (auto& e : ev) (void)hipEventDestroy(e);
   if (rc != GPT_OK) return rc;
   s->steps_done += cnt;
   if (avg_us) *avg_us = 1000.0 * tot / (double)cnt;
@@ -667,6 +686,46 @@ extern "C" int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int6
   HIPCHK(hipStreamSynchronize(s->stream));
   HIPCHK(hipMemcpy(out, buf.p, 8 * per * cnt, hipMemcpyDeviceToHost));
   s->steps_done += cnt;
+  return GPT_OK;
+}
+
+extern "C" int64_t gpt_sgld_timeline_slots(void) { return kTimeline; }
+
+extern "C" int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, int64_t* out,
+                                         double* event_us) {
+  if (!s || !out) { set_error("null argument"); return GPT_ERR_BAD_DIMS; }
+  if (s->engine != kEngineChain) { set_error("timeline: chain engine only"); return GPT_ERR_BAD_DIMS; }
+  const long long left = s->total_steps - s->steps_done;
+  const int span = session_span(s, s->steps_done, std::min<long long>(nsteps, left));
+  if (nsteps < 1 || span != nsteps || nsteps > kTimelineSteps) {
+    set_error("timeline: nsteps must be one launch (within the epoch and the run, <= 512)");
+    return GPT_ERR_BAD_DIMS;
+  }
+  const size_t per = (size_t)kTimeline * s->nchains;
+  DevMem buf;
+  HIPCHK(buf.alloc(8 * per));
+  HIPCHK(hipMemsetAsync(buf.p, 0, 8 * per, s->stream));
+  StepParams P = s->P;
+  P.stamps = buf.as<long long>();
+  s->ran = true;
+  hipError_t eo = session_epoch_order(s, s->steps_done, 0);
+  if (eo != hipSuccess) return hip_fail(eo, "launch_epoch_order");
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  hipError_t e = hipEventRecord(e0, s->stream);
+  if (e == hipSuccess) e = session_launch(s, P, 0, (int)nsteps);
+  if (e == hipSuccess) e = hipEventRecord(e1, s->stream);
+  if (e == hipSuccess) e = launch_advance(s->tbase.as<long long>(), nsteps, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  float ms = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (e != hipSuccess) return hip_fail(e, "timeline launch");
+  if (event_us) *event_us = 1000.0 * ms;
+  HIPCHK(hipMemcpy(out, buf.p, 8 * per, hipMemcpyDeviceToHost));
+  s->steps_done += nsteps;
   return GPT_OK;
 }
 
@@ -752,10 +811,7 @@ extern "C" int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double
 extern "C" void gpt_sgld_session_destroy(gpt_sgld_session* s) {
   if (!s) return;
   (void)hipStreamSynchronize(s->stream);
-  for (auto& g : s->graphs) {
-    (void)hipGraphExecDestroy(g.x);
-    (void)hipGraphDestroy(g.g);
-  }
+  session_drop_graphs(s);
   if (s->own_stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }

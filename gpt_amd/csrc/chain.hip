@@ -91,18 +91,37 @@ struct ChainLds {
   static constexpr int bytes = al16c(o_un + 8 * (L_dbl > x_dbl * WV ? L_dbl : x_dbl * WV));
 };
 
+#ifndef CHAIN_TIMELINE            // diagnostic builds only (make timeline): per-step timeline
+#define CHAIN_TIMELINE 0          // of every workgroup in P.stamps (kTimeline slots per block)
+#endif
+
 // Diagnostic phase stamps (gpt_sgld_session_stamps only): s_memtime of wave 0 at phase ends.
+#if CHAIN_TIMELINE
+#define CSTAMP(slot) do {} while (0)
+// slot i of the block's timeline: {s_memrealtime (100 MHz constant clock), s_memtime (shader
+// clock)}; 0 = entry, 1 = prologue end, 2 + s = end of the launch's step s
+#define TSTAMP(i)                                                                           \
+  do {                                                                                      \
+    if (P.stamps && tid == 0 && (i) < kTimelineSteps + 2) {                                 \
+      long long* ts_ = P.stamps + (size_t)blockIdx.x * kTimeline + 2 * (i);                 \
+      ts_[0] = (long long)__builtin_amdgcn_s_memrealtime();                                \
+      ts_[1] = (long long)__builtin_amdgcn_s_memtime();                                    \
+    }                                                                                       \
+  } while (0)
+#else
 #define CSTAMP(slot)                                                                        \
   do {                                                                                      \
     if (P.stamps && tid == 0)                                                               \
       P.stamps[(size_t)blockIdx.x * kStamps + (slot)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
+#define TSTAMP(i) do {} while (0)
+#endif
 
 // Loop sub-phase stamps (diagnostic runs only): waves 0 and 4 (one SIMD) at one row group, in the
 // stamp row gridDim.x + blockIdx.x (the library sizes the stamp buffer for D+1 rows per chain).
 #define LSTAMP(slot)                                                                        \
   do {                                                                                      \
-    if (P.stamps && g0 == 20 && lane == 0 && (k == 0 || k == 4))                            \
+    if (!CHAIN_TIMELINE && P.stamps && g0 == 20 && lane == 0 && (k == 0 || k == 4))                            \
       P.stamps[(size_t)(gridDim.x + blockIdx.x) * kStamps + (k ? 8 : 0) + (slot)] =         \
           (long long)__builtin_amdgcn_s_memtime();                                         \
   } while (0)
@@ -160,6 +179,14 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   // steps t0 .. tend-1 of this chain in one launch (a chunk of at most one epoch): U^(k) stays in
   // registers and w in LDS between steps; the next batch's rows and targets are fetched during
   // the previous step's Stiefel phase
+  TSTAMP(0);
+#if CHAIN_TIMELINE
+  if (P.stamps && tid == 0) {           // where the workgroup runs: HW_ID and XCC_ID
+    long long* ts_ = P.stamps + (size_t)blockIdx.x * kTimeline + kTimeline - 2;
+    ts_[0] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    ts_[1] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+  }
+#endif
   const long long t0 = tbase[0] + t_local;
   if (t0 >= P.total_steps) return;
   if (__hip_atomic_load(Cp->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
@@ -263,6 +290,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   }
   __syncthreads();
   CSTAMP(1);
+  TSTAMP(1);
 
 
 
@@ -749,7 +777,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       }
     }
     SSTAMP(13);
-    if (P.stamps && lane == 0)            // per-wave arrival at the end-of-step barrier (diag)
+    if (!CHAIN_TIMELINE && P.stamps && lane == 0)   // per-wave arrival at the end-of-step barrier
     P.stamps[(size_t)blockIdx.x * kStamps + 8 + k] = (long long)__builtin_amdgcn_s_memtime();
   if (CHAIN_SPRIO == 2) __builtin_amdgcn_s_setprio(0);
   __syncthreads();                      // w_l, flag and the gradw partials are complete
@@ -776,6 +804,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     }
     CSTAMP(7);
     SSTAMP(15);
+    TSTAMP(2 + (int)(t - t0));
     if (++t >= tend) break;
     ord = ordn;
     Bt = Bn;

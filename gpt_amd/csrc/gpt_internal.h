@@ -59,6 +59,8 @@ struct StepParams {
   double rms_eps, rms_alpha;      // its epsilon and moving-average coefficient
 };
 constexpr int kStamps = 16;       // stamp slots per block
+constexpr int kTimelineSteps = 512;                 // timeline diagnostics: steps per launch
+constexpr int kTimeline = 2 * (kTimelineSteps + 2) + 2;   // int64 per block (+ HW_ID, XCC_ID)
 constexpr double kRmsLambda = 1e-5;   // RMSprop smoothing (GPT_SGLD.jl:1146)
 
 GPT_HD size_t al16(size_t x) { return (x + 15) & ~size_t(15); }

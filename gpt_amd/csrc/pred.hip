@@ -533,10 +533,14 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
                                    const double* phitest, int n, int D, long long Ntest, int r,
                                    int Q, int S, double* fhat, hipStream_t st,
                                    PredPhaseTiming* timing) {
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  struct Events {                          // destroyed on every exit path
+    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+    ~Events() { for (auto x : e) if (x) (void)hipEventDestroy(x); }
+  } evs;
+  hipEvent_t* ev = evs.e;
   if (timing)
-    for (auto& x : ev) {
-      const hipError_t ee = hipEventCreate(&x);
+    for (int i = 0; i < 3; ++i) {
+      const hipError_t ee = hipEventCreate(&ev[i]);
       if (ee != hipSuccess) return ee;
     }
   // temp of up to ~2 GiB of samples per pass; a pass of several workgroup tiles takes a multiple of
@@ -642,8 +646,6 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     }
   }
   hipError_t ef = hipFreeAsync(T, st);
-  if (timing)
-    for (auto& x : ev) (void)hipEventDestroy(x);
   return e != hipSuccess ? e : ef;
 }
 

@@ -150,6 +150,12 @@ int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, double* avg
 /* Diagnostic: run nsteps un-captured steps recording s_memtime (shader-clock ticks)
  * stamps per phase; out = nsteps x (D+1)*nchains x 16 int64 (0 = phase not reached). */
 int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out);
+/* Diagnostic (chain engine, the timeline build `make timeline`; the product library writes
+ * nothing): ONE launch of nsteps steps (within the current epoch, <= 512); out = nchains x
+ * gpt_sgld_timeline_slots() int64: per block {s_memrealtime, s_memtime} at entry, prologue end
+ * and the end of every step, then HW_ID and XCC_ID.  *event_us = the launch's hipEvent time. */
+int64_t gpt_sgld_timeline_slots(void);
+int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, int64_t* out, double* event_us);
 /* Copy chain c's stores / status back (status: GPT_OK or GPT_ERR_NAN_GEODESIC). */
 int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double* w_store, double* U_store,
                            double* diag, int32_t* status);

@@ -57,9 +57,11 @@ import bench
 dist.init_process_group("gloo")
 rank = dist.get_rank()
 dt = bench.max_over_ranks(0.5 + rank)          # rank r 'took' 0.5 + r seconds
+kus = bench.gather_over_ranks(90.0 + rank)     # per-rank kernel time in the line
+seeds = bench.chain_seeds(rank, 1000)
 with open(os.path.join(%r, "rank%%d.json" %% rank), "w") as f:
     json.dump(dict(rank=rank, world=dist.get_world_size(), local=int(os.environ["LOCAL_RANK"]),
-                   dt=dt, argv=sys.argv[1:]), f)
+                   dt=dt, argv=sys.argv[1:], kus=kus, seeds=seeds), f)
 dist.destroy_process_group()
 """
 
@@ -92,3 +94,42 @@ def test_bench_self_launch_gloo_world2(tmp_path):
     assert sorted(g["rank"] for g in got) == [0, 1]
     assert all(g["world"] == 2 and g["dt"] == 1.5 and g["argv"] == ["--steps", "3"] for g in got)
     assert sorted(g["local"] for g in got) == [0, 1]
+    assert all(g["kus"] == [90.0, 91.0] for g in got)
+    # 1000 chains per rank: the seeds of the two ranks do not collide (round-2 seeds did)
+    assert len(set(got[0]["seeds"]) | set(got[1]["seeds"])) == 2000
+
+
+def test_chain_seeds_distinct_over_ranks():
+    import bench
+    for C in (1, 7, 256, 1000, 1024):
+        allseeds = [s for rk in range(8) for s in bench.chain_seeds(rk, C)]
+        scratch = [s for rk in range(8) for s in bench.scratch_seeds(rk, C)]
+        assert len(set(allseeds)) == 8 * C and len(set(scratch)) == 8 * C
+        assert not set(allseeds) & set(scratch)
+
+
+def test_bench_line_fields_at_world_2():
+    """The rank-0 line of an N = 2 run carries the same fields as N = 1: cpu_baseline, per-rank
+    kernel times, the single-chain pass (a SCALE line has what a BENCH line has)."""
+    import types
+    import bench
+    args = types.SimpleNamespace(workload="kin40k", steps=20, warmup=5, epsw=1e-5, epsU=1e-8,
+                                 signal_var=0.0476)
+    quality = dict(test_rmse=0.28, note="x")
+    common = dict(args=args, value=5.0e6, warm_ms=300.0, ms_per_step=0.1, wdesc="kin40k", N=10000,
+                  Nte=30000, D=8, n=500, r=5, Q=200, m=50, C=256,
+                  info=dict(engine="chain", workgroups=256, threads=512, lds_bytes=73600),
+                  achieved=5000.0, traffic=4.2e8, traffic_src="t", bytes_launch=4.94e8,
+                  steps_run=41000, cpu=dict(value=17000.0, cores=16, kind="port"),
+                  quality=quality, allreduce_ms=0.05, npred=256, pred_ms=6.9, pred_flop=3.07e11,
+                  gemm_ms=5.4, vphase_ms=1.0, rmse_final=0.28,
+                  single=dict(steps_per_s=2e4, kernel_us=50.0))
+    one = bench.compose_line(types.SimpleNamespace(world=1, world_seen=1, k_us=93.0,
+                                                   k_us_ranks=[93.0], **common))
+    two = bench.compose_line(types.SimpleNamespace(world=2, world_seen=2, k_us=93.0,
+                                                   k_us_ranks=[93.0, 94.0], **common))
+    assert set(one) == set(two) and set(one["roofline"]) == set(two["roofline"])
+    assert two["n_gpus"] == 2 and two["cpu_baseline"]["cores"] == 16
+    assert two["roofline"]["kernel_us_per_rank"] == [93.0, 94.0]
+    assert two["single_chain"]["steps_per_s"] == 2e4
+    assert two["config"]["parallelism"] == "chains256x2"

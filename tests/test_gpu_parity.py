@@ -276,6 +276,31 @@ def test_rmsprop_trajectory_matches_oracle(name):
     assert rel(dg[1:], np.array(info["gradU_norm"]).T) < 1e-9
 
 
+def test_rmsprop_set_after_prepare_runs_rmsprop_steps():
+    """Graphs prepared before set_rmsprop captured plain SGLD steps; set_rmsprop drops them, so
+    the run that follows takes RMSprop steps (the stale graphs used to be replayed)."""
+    import torch
+    from gpt_amd.session import SGLDSession
+    n, D, N, r, Q, m, burnin, maxepoch, eps = RMS_CASES["small"]
+    p = make_problem(n, D, N, r, Q, seed=13)
+    alpha, sv, seed = 0.9, 0.05, 29
+    dev = torch.device("cuda", 0)
+    phi = torch.from_numpy(np.ascontiguousarray(np.asarray(p["phi"]).transpose(2, 1, 0))).to(dev)
+    y = torch.from_numpy(np.ascontiguousarray(np.asarray(p["y"], dtype=np.float64))).to(dev)
+    s = SGLDSession(phi, y, p["I"], r, Q, m, eps, eps, sv, burnin, maxepoch, [seed],
+                    engine="grid")
+    s.prepare(s.total_steps)
+    s.set_rmsprop(eps, alpha)
+    s.run(s.total_steps)
+    ws, Us, st = s.fetch(0)
+    s.close()
+    wo, Uo, info = R.GPT_SGLDERM_RMSprop(p["phi"], p["y"], sv, p["I"], r, Q, m, eps, alpha, burnin,
+                                         maxepoch, seed)
+    assert st == 0 and info["status"] == 0
+    assert rel(ws, wo) < 1e-8, rel(ws, wo)
+    assert rel(Us, Uo) < 1e-8, rel(Us, Uo)
+
+
 def test_pred_mean_x_fused_features():
     """Fused feature+pred (§8(f) per-epoch evaluation) equals pred_mean over materialised
     features, and the per-sample RMSE curve matches the oracle."""
