@@ -1,6 +1,7 @@
 # GPT_SGLD_HIP — drop-in replacement of the reference's `GPT_SGLD` module entry points on the
-# MI355X path, via `ccall` into libgptsgld.so (include/gptsgld.h).  Untested here (no Julia on the
-# image); mirrors the Python binding gpt_amd/GPT_SGLD.py, which is tested.
+# MI355X path, via `ccall` into libgptsgld.so (include/gptsgld.h).  Julia is not on the image:
+# tests/test_julia_shim.py checks every ccall against the C prototypes, and the Python binding
+# gpt_amd/GPT_SGLD.py (tested on the GPU) makes the identical C calls.
 #
 #   kin40kExperiment.jl:  `@everywhere using GPT_SGLD`  ->  `@everywhere using GPT_SGLD_HIP`
 #
@@ -9,7 +10,8 @@
 module GPT_SGLD_HIP
 
 export datawhitening, feature, featureNotensor, samplenz, GPTregression, GPT_SGLDERM, pred, RMSE,
-       GPNT_SGLD, GPT_SGLDERM_RMSprop, GPT_SGLDERMw, GPTclassification, GPT_GMC
+       GPNT_SGLD, GPT_SGLDERM_RMSprop, GPT_SGLDERMw, GPTclassification, GPT_GMC, pred_mean_x,
+       init_state
 
 const LIB = get(ENV, "GPTSGLD_LIB", joinpath(@__DIR__, "..", "gpt_amd", "libgptsgld.so"))
 
@@ -77,6 +79,19 @@ function featureNotensor(X::Array{Float64,2}, length_scale, sigma_RBF::Real, Z::
                  Ptr{Float64}, Int64, Ptr{Float64}),
                 X, N, D, ls, length(ls), sigma_RBF, Z, b, n, phi))
     return phi
+end
+
+# Generation-C seeded form featureNotensor(X,n,length_scale,sigma_RBF,seed), the call of
+# PowerPlantNoTensorExperiment.jl:32-33, kin40kNoTensorExperiment.jl:35-36 and
+# PowerPlantDataExperiment.jl:159: Z = randn(n,D), b = 2π·rand(n) drawn by gpt_feature_inputs on
+# the framework's Philox contract (column 1 of its b), then the Gen-D map above
+function featureNotensor(X::Array{Float64,2}, n::Integer, length_scale, sigma_RBF::Real,
+                         seed::Integer)
+    D = size(X, 2)
+    Z = Array{Float64}(undef, n, D); b = Array{Float64}(undef, n, D)
+    check(ccall((:gpt_feature_inputs, LIB), Cint, (Int64, Int64, UInt64, Ptr{Float64}, Ptr{Float64}),
+                n, D, seed, Z, b))
+    return featureNotensor(X, length_scale, sigma_RBF, Z, b[:, 1])
 end
 
 # samplenz(r,D,Q,seed)  GPT_SGLD_p.jl:57
@@ -214,6 +229,35 @@ function RMSE(w_store::Array{Float64,2}, U_store::Array{Float64,4}, I::Array{Int
                  Int64, Int64, Int64, Float64, Ptr{Float64}, Ref{Float64}),
                 w_store, U_store, I, phitest, vec(ytest), n, D, Nt, r, Q, S, 1.0, meanf, out))
     return out[]
+end
+
+# The per-epoch evaluation of kin40kExperiment.jl:78-87 with the test features formed inside the
+# prediction kernel (no n·D·Ntest phitest array): returns (meanfhat, scale·RMSE of the mean,
+# per-sample scale·RMSE = the testRMSE curve when the samples are the epoch ends)
+function pred_mean_x(w_store::Array{Float64,2}, U_store::Array{Float64,4}, I::Array{Int32,2},
+                     Xtest::Array{Float64,2}, ytest::Array{Float64}, length_scale,
+                     sigma_RBF::Real, phi_scale::Real, Z::Array{Float64,2}, b::Array{Float64};
+                     scale::Real=1.0)
+    Nt, D = size(Xtest); n = size(Z, 1); r = size(U_store, 2); Q, S = size(w_store)
+    ls = collect(Float64, length_scale isa Real ? [length_scale] : length_scale)
+    meanf = Array{Float64}(undef, Nt); out = Ref(0.0); curve = Array{Float64}(undef, S)
+    check(ccall((:gpt_pred_mean_x, LIB), Cint,
+                (Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64}, Int64, Int64,
+                 Ptr{Float64}, Int64, Float64, Float64, Ptr{Float64}, Ptr{Float64}, Int64, Int64,
+                 Int64, Int64, Float64, Ptr{Float64}, Ref{Float64}, Ptr{Float64}),
+                w_store, U_store, I, Xtest, vec(ytest), Nt, D, ls, length(ls), sigma_RBF,
+                phi_scale, Z, b, n, r, Q, S, scale, meanf, out, curve))
+    return meanf, out[], curve
+end
+
+# The initial draws of GPTregression for param_seed (GPT_SGLD.jl:357-369): (w, U)
+function init_state(n::Integer, r::Integer, D::Integer, Q::Integer, param_seed::Integer;
+                    stiefel=true, sigma_w::Real=1.0)
+    cfg = Ref(SGLDConfig(n, D, 1, r, Q, 1, 0.0, 0.0, 1.0, sigma_w, 0, 1, UInt64(param_seed),
+                         Int32(1), Int32(stiefel), 1, 0))
+    w = Array{Float64}(undef, Q); U = Array{Float64}(undef, n, r, D)
+    check(ccall((:gpt_sgld_init, LIB), Cint, (Ref{SGLDConfig}, Ptr{Float64}, Ptr{Float64}), cfg, w, U))
+    return w, U
 end
 
 # GPNT_SGLD(phi,y,signal_var,sigma_theta,m,eps_theta,decay_rate,burnin,maxepoch,param_seed)

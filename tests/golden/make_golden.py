@@ -48,6 +48,9 @@ def main(ref):
     with h5py.File(os.path.join(ref, "testRMSE_PP.h5"), "r") as f:
         curves["testRMSE_PP"] = f["testRMSE"][()]
         curves["testRMSE2_PP"] = f["testRMSE2"][()]
+    with h5py.File(os.path.join(ref, "fullWresults.h5"), "r") as f:     # GPT_fullw_gibbs curves
+        curves["fullW_testRMSE"] = f["testRMSE"][()]
+        curves["fullW_trainRMSE"] = f["trainRMSE"][()]
     np.savez(os.path.join(out, "ref_curves.npz"), **curves)
     print("wrote fixtures to", out)
 
