@@ -23,6 +23,15 @@ namespace gpt {
 #ifndef CHAIN_EXP_NOSTAGE        // diagnostics only (wrong results): skip the row DMA / V tasks
 #define CHAIN_EXP_NOSTAGE 0
 #endif
+#ifndef CHAIN_EXP_NONOISE        // ablations (wrong results; scripts/ablation.sh): no U-noise draws,
+#define CHAIN_EXP_NONOISE 0       // Box–Muller on a hash instead of Philox, no expm
+#endif
+#ifndef CHAIN_EXP_NOPHILOX
+#define CHAIN_EXP_NOPHILOX 0
+#endif
+#ifndef CHAIN_EXP_NOEXPM
+#define CHAIN_EXP_NOEXPM 0
+#endif
 #ifndef CHAIN_EXP_NOV
 #define CHAIN_EXP_NOV 0
 #endif
@@ -95,42 +104,66 @@ struct ChainLds {
 #define CHAIN_TIMELINE 0          // of every workgroup in P.stamps (kTimeline slots per block)
 #endif
 
-// Diagnostic phase stamps (gpt_sgld_session_stamps only): s_memtime of wave 0 at phase ends.
+#ifndef CHAIN_SSTAMP
+#define CHAIN_SSTAMP 0            // diagnostic builds only (make diag): Stiefel sub-phase stamps
+#endif
+// Phase / loop stamps (written only when P.stamps is set, gpt_sgld_session_stamps).  They stay
+// compiled into the product kernel: without them (CHAIN_STAMPS=0, or sched_barrier fences in
+// their place, CHAIN_SCHED_FENCE=1) the allocator of this 256-VGPR kernel ends at 65-69 spilled
+// VGPRs instead of 20, ten of them reloaded inside the batch loop (round-3 experiment).
+#ifndef CHAIN_STAMPS
+#define CHAIN_STAMPS 1
+#endif
+#ifndef CHAIN_SCHED_FENCE
+#define CHAIN_SCHED_FENCE 0
+#endif
+#if CHAIN_SCHED_FENCE
+#define CHAIN_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define CHAIN_FENCE() do {} while (0)
+#endif
+#if !CHAIN_STAMPS
+#define CSTAMP(slot) CHAIN_FENCE()
+#endif
 #if CHAIN_TIMELINE
-#define CSTAMP(slot) do {} while (0)
 // slot i of the block's timeline: {s_memrealtime (100 MHz constant clock), s_memtime (shader
-// clock)}; 0 = entry, 1 = prologue end, 2 + s = end of the launch's step s
+// clock)}; 0 = entry, 1 = prologue end, 2 + s = end of the launch's step s.  The timeline sits
+// after the phase-stamp rows (2·kStamps per chain), whose code stays as in the product kernel.
 #define TSTAMP(i)                                                                           \
   do {                                                                                      \
     if (P.stamps && tid == 0 && (i) < kTimelineSteps + 2) {                                 \
-      long long* ts_ = P.stamps + (size_t)blockIdx.x * kTimeline + 2 * (i);                 \
+      long long* ts_ = P.stamps + (size_t)gridDim.x * 2 * kStamps +                        \
+                       (size_t)blockIdx.x * kTimeline + 2 * (i);                            \
       ts_[0] = (long long)__builtin_amdgcn_s_memrealtime();                                \
       ts_[1] = (long long)__builtin_amdgcn_s_memtime();                                    \
     }                                                                                       \
   } while (0)
 #else
+#define TSTAMP(i) do {} while (0)
+#endif
+#if CHAIN_STAMPS
 #define CSTAMP(slot)                                                                        \
   do {                                                                                      \
     if (P.stamps && tid == 0)                                                               \
       P.stamps[(size_t)blockIdx.x * kStamps + (slot)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
-#define TSTAMP(i) do {} while (0)
 #endif
 
 // Loop sub-phase stamps (diagnostic runs only): waves 0 and 4 (one SIMD) at one row group, in the
 // stamp row gridDim.x + blockIdx.x (the library sizes the stamp buffer for D+1 rows per chain).
+#if CHAIN_STAMPS
 #define LSTAMP(slot)                                                                        \
   do {                                                                                      \
-    if (!CHAIN_TIMELINE && P.stamps && g0 == 20 && lane == 0 && (k == 0 || k == 4))                            \
+    if (P.stamps && g0 == 20 && lane == 0 && (k == 0 || k == 4))                            \
       P.stamps[(size_t)(gridDim.x + blockIdx.x) * kStamps + (k ? 8 : 0) + (slot)] =         \
           (long long)__builtin_amdgcn_s_memtime();                                         \
   } while (0)
+#else
+#define LSTAMP(slot) CHAIN_FENCE()
+#endif
 
 // Stiefel sub-phase stamps (diagnostic runs only): waves 0 and 4 of every step, slot i < 16 in
 // stamp row (2 + i/8)·gridDim.x + blockIdx.x (columns i%8, +8 for wave 4).
-#ifndef CHAIN_SSTAMP
-#define CHAIN_SSTAMP 0            // diagnostic builds only (make diag): Stiefel sub-phase stamps
-#endif
 #define SSTAMP(slot)                                                                        \
   do {                                                                                      \
     if (CHAIN_SSTAMP && P.stamps && lane == 0 && (k == 0 || k == 4))                                        \
@@ -182,7 +215,8 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   TSTAMP(0);
 #if CHAIN_TIMELINE
   if (P.stamps && tid == 0) {           // where the workgroup runs: HW_ID and XCC_ID
-    long long* ts_ = P.stamps + (size_t)blockIdx.x * kTimeline + kTimeline - 2;
+    long long* ts_ = P.stamps + (size_t)gridDim.x * 2 * kStamps + (size_t)blockIdx.x * kTimeline +
+                     kTimeline - 2;
     ts_[0] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     ts_[1] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
@@ -604,8 +638,23 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 #pragma unroll
       for (int q = 0; q < NQJ; ++q) {
         double z[4];
-        normal_quad<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
-                        (uint32_t)k, z);
+        if (CHAIN_EXP_NONOISE) {
+          z[0] = z[1] = z[2] = z[3] = 0.0;
+        } else if (CHAIN_EXP_NOPHILOX) {
+          const uint32_t h = (uint32_t)((l * NQ + q) * 64 + lane) * 2654435761u ^ (uint32_t)t;
+          const U4 x{h, h * 747796405u, h ^ 0x9E3779B9u, h * 2891336453u};
+          const auto c = fm_coef();
+          const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.x), c));
+          double sn, cs;
+          fm_sincos_2pi_c(u32u(x.y), sn, cs, c);
+          z[0] = rad * cs; z[1] = rad * sn;
+          const double rad2 = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.z), c));
+          fm_sincos_2pi_c(u32u(x.w), sn, cs, c);
+          z[2] = rad2 * cs; z[3] = rad2 * sn;
+        } else {
+          normal_quad<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
+                          (uint32_t)k, z);
+        }
 #pragma unroll
         for (int i = 0; i < NZ; ++i)
           if (4 * q + i < J) xi_l[(4 * q + i) * 64 + lane] = z[i];
@@ -700,7 +749,13 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       wave_sync();
       long long* xst = (CHAIN_SSTAMP && P.stamps && k == 0)
                            ? P.stamps + (size_t)(4 * gridDim.x + blockIdx.x) * kStamps : nullptr;
-      const bool bad = wave_expm<NN>(X0, xst);
+      bool bad = false;
+      if (CHAIN_EXP_NOEXPM) {                 // ablation: E = the input (no Padé)
+        for (int o = lane; o < NN * NN; o += 64) X0[NN * NN + o] = X0[o];
+        wave_sync();
+      } else {
+        bad = wave_expm<NN>(X0, xst);
+      }
       SSTAMP(7);
       for (int o = lane; o < NN * R; o += 64) {
         const int a = o / R, l = o - a * R;
@@ -710,7 +765,12 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       double* X1 = X0;                        // expm(−tA) in the same scratch
       for (int o = lane; o < R * R; o += 64) X1[o] = -tt * Ag[o];
       wave_sync();
-      wave_expm<R>(X1, xst ? xst + (size_t)gridDim.x * kStamps : nullptr);
+      if (CHAIN_EXP_NOEXPM) {
+        for (int o = lane; o < R * R; o += 64) X1[R * R + o] = X1[o];
+        wave_sync();
+      } else {
+        wave_expm<R>(X1, xst ? xst + (size_t)gridDim.x * kStamps : nullptr);
+      }
       if (bad && lane == 0) flag[0] = 1;
       CSTAMP(6);
       SSTAMP(8);
@@ -777,7 +837,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       }
     }
     SSTAMP(13);
-    if (!CHAIN_TIMELINE && P.stamps && lane == 0)   // per-wave arrival at the end-of-step barrier
+    if (CHAIN_STAMPS && P.stamps && lane == 0)   // per-wave arrival at the end-of-step barrier
     P.stamps[(size_t)blockIdx.x * kStamps + 8 + k] = (long long)__builtin_amdgcn_s_memtime();
   if (CHAIN_SPRIO == 2) __builtin_amdgcn_s_setprio(0);
   __syncthreads();                      // w_l, flag and the gradw partials are complete
