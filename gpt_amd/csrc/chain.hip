@@ -107,12 +107,13 @@ struct ChainLds {
 #ifndef CHAIN_SSTAMP
 #define CHAIN_SSTAMP 0            // diagnostic builds only (make diag): Stiefel sub-phase stamps
 #endif
-// Phase / loop stamps (written only when P.stamps is set, gpt_sgld_session_stamps).  They stay
-// compiled into the product kernel: without them (CHAIN_STAMPS=0, or sched_barrier fences in
-// their place, CHAIN_SCHED_FENCE=1) the allocator of this 256-VGPR kernel ends at 65-69 spilled
-// VGPRs instead of 20, ten of them reloaded inside the batch loop (round-3 experiment).
+// Phase / loop stamps (gpt_sgld_session_stamps): compiled into the diagnostic builds only.  The
+// product kernel without them takes 217 k instead of 236 k shader cycles per 256-chain step
+// (scripts/ablation_run.py, round 3) although the allocator then reports 65 spilled VGPRs
+// instead of 20: the stamps' branches split the step into blocks the scheduler could not
+// overlap across.
 #ifndef CHAIN_STAMPS
-#define CHAIN_STAMPS 1
+#define CHAIN_STAMPS CHAIN_SSTAMP
 #endif
 #ifndef CHAIN_SCHED_FENCE
 #define CHAIN_SCHED_FENCE 0
@@ -129,7 +130,7 @@ struct ChainLds {
 // slot i of the block's timeline: {s_memrealtime (100 MHz constant clock), s_memtime (shader
 // clock)}; 0 = entry, 1 = prologue end, 2 + s = end of the launch's step s.  The timeline sits
 // after the phase-stamp rows (2·kStamps per chain), whose code stays as in the product kernel.
-#define TSTAMP(i)                                                                           \
+#define TSTAMP_ANY(i)                                                                       \
   do {                                                                                      \
     if (P.stamps && tid == 0 && (i) < kTimelineSteps + 2) {                                 \
       long long* ts_ = P.stamps + (size_t)gridDim.x * 2 * kStamps +                        \
@@ -138,6 +139,13 @@ struct ChainLds {
       ts_[1] = (long long)__builtin_amdgcn_s_memtime();                                    \
     }                                                                                       \
   } while (0)
+#else
+#define TSTAMP_ANY(i) do {} while (0)
+#endif
+// CHAIN_TIMELINE = 1: every step end; = 2: entry, prologue end and the launch's last step end only
+// (no stamp code inside the step loop, so the loop compiles as in the product kernel)
+#if CHAIN_TIMELINE == 1
+#define TSTAMP(i) TSTAMP_ANY(i)
 #else
 #define TSTAMP(i) do {} while (0)
 #endif
@@ -212,7 +220,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   // steps t0 .. tend-1 of this chain in one launch (a chunk of at most one epoch): U^(k) stays in
   // registers and w in LDS between steps; the next batch's rows and targets are fetched during
   // the previous step's Stiefel phase
-  TSTAMP(0);
+  TSTAMP_ANY(0);
 #if CHAIN_TIMELINE
   if (P.stamps && tid == 0) {           // where the workgroup runs: HW_ID and XCC_ID
     long long* ts_ = P.stamps + (size_t)gridDim.x * 2 * kStamps + (size_t)blockIdx.x * kTimeline +
@@ -324,7 +332,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   }
   __syncthreads();
   CSTAMP(1);
-  TSTAMP(1);
+  TSTAMP_ANY(1);
 
 
 
@@ -869,6 +877,9 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     ord = ordn;
     Bt = Bn;
   }
+#if CHAIN_TIMELINE == 2
+  TSTAMP_ANY(2 + (int)(tend - 1 - t0));
+#endif
 }
 
 // ------------------------------------------------------------------------------ host side

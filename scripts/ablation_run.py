@@ -39,9 +39,10 @@ s.run(200); s.sync()                      # warm-up epoch (clock, caches)
 out = np.zeros((Cn, S), dtype=np.int64)
 ev = C.c_double(0.0)
 check(lib().gpt_sgld_session_timeline(s._h, 200, out.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(ev)))
-rt = out[:, 2:2 * 202:2].astype(float); mt = out[:, 3:2 * 202:2].astype(float)
-cyc = np.diff(mt, axis=1)                 # per chain, per step (prologue end -> step ends)
-us = np.diff(rt, axis=1) / 100.0
+# slots: 0 entry, 1 prologue end, 2 + s end of step s (CHAIN_TIMELINE=2 builds: the last only)
+rt = out[:, [2, 2 * 201]].astype(float); mt = out[:, [3, 2 * 201 + 1]].astype(float)
+cyc = np.diff(mt, axis=1) / 200.0         # per chain: prologue end -> last step end, per step
+us = np.diff(rt, axis=1) / 100.0 / 200.0
 print(json.dumps(dict(cycles_per_step_median=float(np.median(cyc)), cycles_per_step_mean=float(cyc.mean()),
                       us_per_step_median=float(np.median(us)), event_us_per_step=ev.value / 200,
                       clock_mhz=float(np.median(cyc / np.maximum(us, 1e-9))))))
