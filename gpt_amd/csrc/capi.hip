@@ -401,6 +401,7 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     P.runq = s->runq.as<int32_t>();
   }
   P.stamps = nullptr;
+  P.tline = nullptr;
   P.rms = 0; P.rms_eps = 0.0; P.rms_alpha = 0.0;
   P.wonly = (store_flags & 16) ? 1 : 0;
   P.ncls = (store_flags & 32) ? nchains : 0;
@@ -701,14 +702,12 @@ extern "C" int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, in
     set_error("timeline: nsteps must be one launch (within the epoch and the run, <= 512)");
     return GPT_ERR_BAD_DIMS;
   }
-  // the kernel's phase-stamp rows (2·kStamps per chain) first, then the timeline
-  const size_t pre = (size_t)2 * kStamps * s->nchains;
   const size_t per = (size_t)kTimeline * s->nchains;
   DevMem buf;
-  HIPCHK(buf.alloc(8 * (pre + per)));
-  HIPCHK(hipMemsetAsync(buf.p, 0, 8 * (pre + per), s->stream));
+  HIPCHK(buf.alloc(8 * per));
+  HIPCHK(hipMemsetAsync(buf.p, 0, 8 * per, s->stream));
   StepParams P = s->P;
-  P.stamps = buf.as<long long>();
+  P.tline = buf.as<long long>();
   s->ran = true;
   hipError_t eo = session_epoch_order(s, s->steps_done, 0);
   if (eo != hipSuccess) return hip_fail(eo, "launch_epoch_order");
@@ -726,7 +725,7 @@ extern "C" int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, in
   (void)hipEventDestroy(e1);
   if (e != hipSuccess) return hip_fail(e, "timeline launch");
   if (event_us) *event_us = 1000.0 * ms;
-  HIPCHK(hipMemcpy(out, buf.as<long long>() + pre, 8 * per, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, buf.p, 8 * per, hipMemcpyDeviceToHost));
   s->steps_done += nsteps;
   return GPT_OK;
 }

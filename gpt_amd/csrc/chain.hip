@@ -23,11 +23,8 @@ namespace gpt {
 #ifndef CHAIN_EXP_NOSTAGE        // diagnostics only (wrong results): skip the row DMA / V tasks
 #define CHAIN_EXP_NOSTAGE 0
 #endif
-#ifndef CHAIN_EXP_NONOISE        // ablations (wrong results; scripts/ablation.sh): no U-noise draws,
-#define CHAIN_EXP_NONOISE 0       // Box–Muller on a hash instead of Philox, no expm
-#endif
-#ifndef CHAIN_EXP_NOPHILOX
-#define CHAIN_EXP_NOPHILOX 0
+#ifndef CHAIN_EXP_NONOISE        // ablations (wrong results; scripts/ablation_build.sh): U noise
+#define CHAIN_EXP_NONOISE 0       // zeroed, no expm
 #endif
 #ifndef CHAIN_EXP_NOEXPM
 #define CHAIN_EXP_NOEXPM 0
@@ -100,8 +97,15 @@ struct ChainLds {
   static constexpr int bytes = al16c(o_un + 8 * (L_dbl > x_dbl * WV ? L_dbl : x_dbl * WV));
 };
 
-#ifndef CHAIN_TIMELINE            // diagnostic builds only (make timeline): per-step timeline
-#define CHAIN_TIMELINE 0          // of every workgroup in P.stamps (kTimeline slots per block)
+// Timeline of every workgroup in P.stamps (gpt_sgld_session_timeline; kTimeline slots per block).
+// 2 (product): entry, prologue end and the launch's last step end, plus HW_ID / XCC_ID — the
+// per-launch dispatch skew, prologue and per-chain span, and shader cycles per step independent
+// of the clock (scripts/ablation_run.py).  The step loop itself carries no stamp code, and this
+// build is also the faster allocation: 217 k shader cycles per 256-chain step and no scratch
+// reload in the batch loop, against 69 spilled VGPRs with ten reloads per row group when the
+// entry / exit stamps are left out too (round 3).  1 (make timeline): every step end as well.
+#ifndef CHAIN_TIMELINE
+#define CHAIN_TIMELINE 2
 #endif
 
 #ifndef CHAIN_SSTAMP
@@ -128,13 +132,11 @@ struct ChainLds {
 #endif
 #if CHAIN_TIMELINE
 // slot i of the block's timeline: {s_memrealtime (100 MHz constant clock), s_memtime (shader
-// clock)}; 0 = entry, 1 = prologue end, 2 + s = end of the launch's step s.  The timeline sits
-// after the phase-stamp rows (2·kStamps per chain), whose code stays as in the product kernel.
+// clock)}; 0 = entry, 1 = prologue end, 2 + s = end of the launch's step s.
 #define TSTAMP_ANY(i)                                                                       \
   do {                                                                                      \
-    if (P.stamps && tid == 0 && (i) < kTimelineSteps + 2) {                                 \
-      long long* ts_ = P.stamps + (size_t)gridDim.x * 2 * kStamps +                        \
-                       (size_t)blockIdx.x * kTimeline + 2 * (i);                            \
+    if (P.tline && tid == 0 && (i) < kTimelineSteps + 2) {                                  \
+      long long* ts_ = P.tline + (size_t)blockIdx.x * kTimeline + 2 * (i);                  \
       ts_[0] = (long long)__builtin_amdgcn_s_memrealtime();                                \
       ts_[1] = (long long)__builtin_amdgcn_s_memtime();                                    \
     }                                                                                       \
@@ -222,9 +224,8 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   // the previous step's Stiefel phase
   TSTAMP_ANY(0);
 #if CHAIN_TIMELINE
-  if (P.stamps && tid == 0) {           // where the workgroup runs: HW_ID and XCC_ID
-    long long* ts_ = P.stamps + (size_t)gridDim.x * 2 * kStamps + (size_t)blockIdx.x * kTimeline +
-                     kTimeline - 2;
+  if (P.tline && tid == 0) {            // where the workgroup runs: HW_ID and XCC_ID
+    long long* ts_ = P.tline + (size_t)blockIdx.x * kTimeline + kTimeline - 2;
     ts_[0] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     ts_[1] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
@@ -648,17 +649,6 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         double z[4];
         if (CHAIN_EXP_NONOISE) {
           z[0] = z[1] = z[2] = z[3] = 0.0;
-        } else if (CHAIN_EXP_NOPHILOX) {
-          const uint32_t h = (uint32_t)((l * NQ + q) * 64 + lane) * 2654435761u ^ (uint32_t)t;
-          const U4 x{h, h * 747796405u, h ^ 0x9E3779B9u, h * 2891336453u};
-          const auto c = fm_coef();
-          const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.x), c));
-          double sn, cs;
-          fm_sincos_2pi_c(u32u(x.y), sn, cs, c);
-          z[0] = rad * cs; z[1] = rad * sn;
-          const double rad2 = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.z), c));
-          fm_sincos_2pi_c(u32u(x.w), sn, cs, c);
-          z[2] = rad2 * cs; z[3] = rad2 * sn;
         } else {
           normal_quad<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
                           (uint32_t)k, z);

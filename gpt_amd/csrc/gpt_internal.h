@@ -52,6 +52,7 @@ struct StepParams {
   const int32_t* runq;            // chain engine: runq[(k*r + l)*64 + s] = s-th q (ascending) with
                                   // I[q,k] = l, or 256 (a zero slot) past the run's end
   long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
+  long long* tline;               // chain engine: per-workgroup timeline (kTimeline per block) or null
   int rms;                        // 1: GPT_SGLDERM_RMSprop steps (grid engine, two launches)
   int wonly;                      // 1: GPT_SGLDERMw steps (w alone, U fixed; grid engine)
   int ncls;                       // >= 2: GPTclassification, chains are the classes of one

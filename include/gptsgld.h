@@ -150,10 +150,11 @@ int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, double* avg
 /* Diagnostic: run nsteps un-captured steps recording s_memtime (shader-clock ticks)
  * stamps per phase; out = nsteps x (D+1)*nchains x 16 int64 (0 = phase not reached). */
 int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out);
-/* Diagnostic (chain engine, the timeline build `make timeline`; the product library writes
- * nothing): ONE launch of nsteps steps (within the current epoch, <= 512); out = nchains x
- * gpt_sgld_timeline_slots() int64: per block {s_memrealtime, s_memtime} at entry, prologue end
- * and the end of every step, then HW_ID and XCC_ID.  *event_us = the launch's hipEvent time. */
+/* Diagnostic (chain engine): ONE launch of nsteps steps (within the current epoch, <= 512);
+ * out = nchains x gpt_sgld_timeline_slots() int64: per block {s_memrealtime, s_memtime} at slot
+ * 0 = entry, 1 = prologue end and 2 + s = end of step s, then HW_ID and XCC_ID.  The product
+ * library fills slots 0, 1 and the last step's; the timeline build (`make timeline`) every step.
+ * *event_us = the launch's hipEvent time. */
 int64_t gpt_sgld_timeline_slots(void);
 int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, int64_t* out, double* event_us);
 /* Copy chain c's stores / status back (status: GPT_OK or GPT_ERR_NAN_GEODESIC). */

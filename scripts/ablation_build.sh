@@ -1,6 +1,6 @@
 #!/bin/bash
 # Chain-engine ablation libraries (CPU side, cross-compiled): chain.hip with entry / exit stamps
-# only (-DCHAIN_TIMELINE=2: the step loop compiles as in the product kernel), one experiment
+# only (CHAIN_TIMELINE=2, the product default: no stamp code in the step loop), one experiment
 # flag each, linked with the other objects
 # of `make timeline`.  Results are wrong by construction; scripts/ablation_run.py measures their
 # shader-clock cycles per step on the GPU (clock-independent).
@@ -14,7 +14,7 @@ others=$(ls build_tl/*.o | grep -v chain.o)
 pids=()
 while [ $# -gt 0 ]; do
   name=$1; extra=$2; shift 2
-  ( /opt/rocm/bin/hipcc $FLAGS -DCHAIN_TIMELINE=2 $extra -c chain.hip -o build_abl/chain_$name.o &&
+  ( /opt/rocm/bin/hipcc $FLAGS $extra -c chain.hip -o build_abl/chain_$name.o &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others build_abl/chain_$name.o \
       -o ../libgptsgld_abl_$name.so && echo "built $name" ) &
   pids+=($!)

@@ -52,7 +52,8 @@ print(json.dumps(dict(cycles_per_step_median=float(np.median(cyc)), cycles_per_s
 def main():
     res = {}
     for name in sys.argv[1:]:
-        lib = os.path.join(ROOT, "gpt_amd", "libgptsgld_abl_%s.so" % name)
+        lib = os.path.join(ROOT, "gpt_amd", "libgptsgld.so" if name == "product"
+                           else "libgptsgld_abl_%s.so" % name)
         env = dict(os.environ, GPTSGLD_LIB=lib)
         p = subprocess.run([sys.executable, "-c", CHILD % dict(root=ROOT)], env=env,
                            capture_output=True, text=True, timeout=240)
