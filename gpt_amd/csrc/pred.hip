@@ -214,7 +214,8 @@ __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __res
                                                              const double* __restrict__ phi,
                                                              int n, int D, int R,
                                                              long long Ntest, int S,
-                                                             double* __restrict__ T) {
+                                                             double* __restrict__ T,
+                                                             long long ldT) {
   constexpr int WC = 32 * TM, WI = 32 * TN;        // workgroup tile (2 × 2 waves of 16TM × 16TN)
   const int SR = S * R;
   const int nct = (SR + WC - 1) / WC;
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __res
         const long long i = iw + 16 * u + (lane & 15);
         if (c < SR && i < Ntest) {
           const int sm = c / R, l = c - sm * R;
-          gptr_w(T)[(((size_t)sm * D + k) * R + l) * (size_t)Ntest + i] = acc[t][u][reg];
+          gptr_w(T)[(((size_t)sm * D + k) * R + l) * (size_t)ldT + i] = acc[t][u][reg];
         }
       }
 }
@@ -431,7 +432,8 @@ __global__ void pred_pair_offs_kernel(const int32_t* __restrict__ I0, int Q, int
 template <int NT>
 __global__ __launch_bounds__(64 * kPairWaves) void pred_vphase_pairs_kernel(
     const double* __restrict__ w, const double* __restrict__ T, const int32_t* __restrict__ offp,
-    int D, int R, long long Ntest, int Q, double* __restrict__ fhat) {
+    int D, int R, long long Ntest, int Q, double* __restrict__ fhat, long long ldT,
+    long long ldF) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* pp = (double*)smem;                                   // [row][64]
   const int tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);
@@ -439,7 +441,7 @@ __global__ __launch_bounds__(64 * kPairWaves) void pred_vphase_pairs_kernel(
   const long long i0 = (long long)blockIdx.x * 64;
   const long long i = i0 + lane;
   const bool ok = i < Ntest;
-  const double* Ts = T + (size_t)s * D * R * Ntest + (ok ? i : i0);
+  const double* Ts = T + (size_t)s * D * R * ldT + (ok ? i : i0);
   const int rows = (D / 2) * R * R + (D & 1) * R;
   double* red = pp + (size_t)rows * 64;
   // tables: wave w builds tables w, w + 4, ..; the 2·R temp rows of a table (512 contiguous
@@ -449,8 +451,8 @@ __global__ __launch_bounds__(64 * kPairWaves) void pred_vphase_pairs_kernel(
     const bool two = 2 * t + 1 < D;
 #pragma unroll
     for (int x = 0; x < 5; ++x) {
-      a[x] = x < R ? gptr(Ts)[(size_t)((2 * t) * R + x) * Ntest] : 0.0;
-      b[x] = (x < R && two) ? gptr(Ts)[(size_t)((2 * t + 1) * R + x) * Ntest] : 1.0;
+      a[x] = x < R ? gptr(Ts)[(size_t)((2 * t) * R + x) * ldT] : 0.0;
+      b[x] = (x < R && two) ? gptr(Ts)[(size_t)((2 * t + 1) * R + x) * ldT] : 1.0;
     }
     double* dst = pp + (size_t)t * R * R * 64 + lane;
     if (two) {
@@ -493,7 +495,7 @@ __global__ __launch_bounds__(64 * kPairWaves) void pred_vphase_pairs_kernel(
     double f = red[lane];
 #pragma unroll
     for (int x = 1; x < kPairWaves; ++x) f += red[x * 64 + lane];
-    fhat[(size_t)s * Ntest + i] = f;
+    fhat[(size_t)s * ldF + i] = f;
   }
 }
 
@@ -506,27 +508,54 @@ static size_t pred_vphase_lds_bytes(int D, int r, int Q) {
 // selects the wave tile (16·TM c × 16·TN i) for comparison runs.
 template <int TM, int TN>
 static void launch_pred_gemm_t(const double* Us, const double* phitest, int n, int D, int r,
-                               long long Ntest, int Sc, double* T, hipStream_t st) {
+                               long long Ntest, int Sc, double* T, hipStream_t st,
+                               long long ldT) {
   const long long total = (long long)((Sc * r + 32 * TM - 1) / (32 * TM)) *
                           ((Ntest + 32 * TN - 1) / (32 * TN)) * D;
   const unsigned grid = (unsigned)((total + kXcds - 1) / kXcds * kXcds);
   if ((n & 1) == 0)
     hipLaunchKernelGGL((pred_temp_mfma_kernel<true, TM, TN>), dim3(grid), dim3(256), 0, st, Us,
-                       phitest, n, D, r, Ntest, Sc, T);
+                       phitest, n, D, r, Ntest, Sc, T, ldT);
   else
     hipLaunchKernelGGL((pred_temp_mfma_kernel<false, TM, TN>), dim3(grid), dim3(256), 0, st, Us,
-                       phitest, n, D, r, Ntest, Sc, T);
+                       phitest, n, D, r, Ntest, Sc, T, ldT);
 }
 
 static hipError_t launch_pred_gemm(const double* Us, const double* phitest, int n, int D, int r,
-                                   long long Ntest, int Sc, double* T, hipStream_t st) {
+                                   long long Ntest, int Sc, double* T, hipStream_t st,
+                                   long long ldT = -1) {
+  if (ldT < 0) ldT = Ntest;
   const char* ev = std::getenv("GPTSGLD_PRED_TILE");
   const int tile = ev ? std::atoi(ev) : 44;
-  if (tile == 22) launch_pred_gemm_t<2, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st);
-  else if (tile == 42) launch_pred_gemm_t<4, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st);
-  else if (tile == 24) launch_pred_gemm_t<2, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st);
-  else launch_pred_gemm_t<4, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st);
+  if (tile == 22) launch_pred_gemm_t<2, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st, ldT);
+  else if (tile == 42) launch_pred_gemm_t<4, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st, ldT);
+  else if (tile == 24) launch_pred_gemm_t<2, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st, ldT);
+  else launch_pred_gemm_t<4, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st, ldT);
   return hipGetLastError();
+}
+
+template <int NN>
+static hipError_t launch_vphase_pairs(const double* w, const double* T, const int32_t* offp, int D,
+                                      int r, long long rows, int Q, double* fhat, int Sc,
+                                      long long ldT, long long ldF, size_t plds, hipStream_t st) {
+  static std::atomic<uint64_t> attr{0};
+  hipError_t e = set_max_lds_once((const void*)pred_vphase_pairs_kernel<NN>, 160 * 1024, attr);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pred_vphase_pairs_kernel<NN>, dim3((unsigned)((rows + 63) / 64), Sc),
+                     dim3(64 * kPairWaves), plds, st, w, T, offp, D, r, rows, Q, fhat, ldT, ldF);
+  return hipGetLastError();
+}
+
+static hipError_t vphase_pairs(int NTp, const double* w, const double* T, const int32_t* offp,
+                               int D, int r, long long rows, int Q, double* fhat, int Sc,
+                               long long ldT, long long ldF, size_t plds, hipStream_t st) {
+  switch (NTp) {
+#define PCASE(NN) \
+    case NN: return launch_vphase_pairs<NN>(w, T, offp, D, r, rows, Q, fhat, Sc, ldT, ldF, plds, st);
+    PCASE(1) PCASE(2) PCASE(3) PCASE(4) PCASE(5) PCASE(6) PCASE(7) PCASE(8)
+#undef PCASE
+    default: return hipErrorInvalidValue;
+  }
 }
 
 static hipError_t launch_pred_mfma(const double* w, const double* U, const int32_t* I0,
@@ -585,20 +614,8 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     if (timing) (void)hipEventRecord(ev[1], st);
     dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
     if (pairs) {
-      switch (NTp) {
-#define PCASE(NN)                                                                              \
-  case NN: {                                                                                   \
-    static std::atomic<uint64_t> attr{0};                                                      \
-    e = set_max_lds_once((const void*)pred_vphase_pairs_kernel<NN>, 160 * 1024, attr);         \
-    if (e != hipSuccess) break;                                                                \
-    hipLaunchKernelGGL(pred_vphase_pairs_kernel<NN>, vg, dim3(64 * kPairWaves), plds, st,      \
-                       w + (size_t)s0 * Q, T, offp, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest);\
-    e = hipGetLastError();                                                                     \
-  } break;
-        PCASE(1) PCASE(2) PCASE(3) PCASE(4) PCASE(5) PCASE(6) PCASE(7) PCASE(8)
-#undef PCASE
-        default: e = hipErrorInvalidValue;
-      }
+      e = vphase_pairs(NTp, w + (size_t)s0 * Q, T, offp, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest,
+                       Sc, Ntest, Ntest, plds, st);
       if (timing && e == hipSuccess) {
         (void)hipEventRecord(ev[2], st);
         (void)hipEventSynchronize(ev[2]);
