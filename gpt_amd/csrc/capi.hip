@@ -208,15 +208,39 @@ struct gpt_sgld_session {
   int graph_steps = 0;                // canonical chunk: one epoch (<= 512 steps)
   DevMem ord_ws;                      // epoch-order workspace when a shuffle exceeds LDS
   bool store = false, diag = false;
-  int engine = 0;                     // kEngineGrid / kEngineChain
+  int engine = 0;                     // kEngineGrid / kEngineChain / kEngineSplit
   DevMem runq;
+  DevMem vtab;                        // grid / split engine: vphase_cols tables
 };
 
-// Engine choice: store_flags bit 2 (or bit 4, w-only steps) forces the grid engine (sgld.hip), bit 3 the chain engine
-// (chain.hip); otherwise GPTSGLD_ENGINE=grid|chain, otherwise chain whenever it supports the shape.
+// Engine choice: store_flags bit 2 (or bit 4, w-only steps) forces the grid engine (sgld.hip), bit 3
+// the chain engine (chain.hip), bit 6 the split engine (sgld.hip, P.split); otherwise
+// GPTSGLD_ENGINE=grid|chain|split, otherwise chain whenever it supports the shape.
 // Without a forced choice, few chains go to the grid engine (D+1 workgroups per chain: the shorter
 // step) as long as every chain's workgroups fit the GPU at once; more chains go to the chain engine
 // (one workgroup per chain, one batch read per step: the higher throughput).
+// Batch slices per dimension of the split engine: the largest S <= 8 whose D·S + 1 workgroups
+// per chain all fit the GPU at once (the in-kernel barrier needs the whole grid resident) with
+// at least 6 rows per slice; GPTSGLD_SPLIT=S overrides (S >= 2, still subject to residency).
+static int split_factor(int nchains, int D, int m, int cus) {
+  int S = 1;
+  for (int s2 = 2; s2 <= 8; ++s2)
+    if ((long long)nchains * (D * s2 + 1) <= cus && m / s2 >= 6) S = s2;
+  if (const char* ev = std::getenv("GPTSGLD_SPLIT")) {
+    const int v = std::atoi(ev);
+    if (v >= 1 && (long long)nchains * (D * v + 1) <= cus) S = v;
+  }
+  return S;
+}
+
+static int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return cus;
+}
+
 static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t flags,
                        int nchains, int* engine) {
   int max_run = 0;                    // longest run of core entries sharing one I[·,k] value
@@ -231,9 +255,18 @@ static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t 
   int want = -1;
   if (flags & (4 | 16 | 32)) want = kEngineGrid;
   else if (flags & 8) want = kEngineChain;
+  else if (flags & 64) want = kEngineSplit;
   else if (const char* ev = std::getenv("GPTSGLD_ENGINE")) {
     if (!std::strcmp(ev, "grid")) want = kEngineGrid;
     else if (!std::strcmp(ev, "chain")) want = kEngineChain;
+    else if (!std::strcmp(ev, "split")) want = kEngineSplit;
+  }
+  if (want == kEngineSplit) {
+    if (!grid_ok) { set_error("split engine: working set exceeds 160 KiB LDS"); return GPT_ERR_BAD_DIMS; }
+    if (split_factor(nchains, (int)c->D, (int)c->m, device_cus()) < 2) {
+      set_error("split engine: D*S + 1 workgroups per chain (S >= 2) do not fit the GPU at once");
+      return GPT_ERR_BAD_DIMS;
+    }
   }
   if (want == kEngineChain && !chain_ok) {
     set_error("chain engine does not support this shape (needs D<=8, r<=5, n<=512 (even if >64), "
@@ -243,13 +276,10 @@ static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t 
   if (want == kEngineGrid && !grid_ok) {
     set_error("grid engine: working set exceeds 160 KiB LDS"); return GPT_ERR_BAD_DIMS;
   }
-  if (want < 0 && chain_ok && grid_ok) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        (long long)nchains * (c->D + 1) <= cus)
-      want = kEngineGrid;
-  }
+  // few chains: the grid engine's D+1 workgroups per chain (the shorter step).  The split engine
+  // stays opt-in: its slices' exchange costs more than the batch work it divides at the
+  // measured shapes (scripts/single_chain.py)
+  if (want < 0 && grid_ok && (long long)nchains * (c->D + 1) <= device_cus()) want = kEngineGrid;
   *engine = want >= 0 ? want : (chain_ok ? kEngineChain : kEngineGrid);
   return GPT_OK;
 }
@@ -303,7 +333,7 @@ static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t
 
 // temp of the first step (grid engine only: the chain engine forms temp inside its step).
 static int session_prime(gpt_sgld_session* s) {
-  if (s->engine != kEngineGrid || s->temp_ready) return GPT_OK;
+  if (s->engine == kEngineChain || s->temp_ready) return GPT_OK;
   hipError_t e = launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
                                   s->tbase.as<long long>(), s->stream);
   if (e != hipSuccess) return hip_fail(e, "launch_temp_init");
@@ -400,11 +430,20 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     HIPCHK(hipMemcpy(s->runq.p, rq.data(), sizeof(int32_t) * rq.size(), hipMemcpyHostToDevice));
     P.runq = s->runq.as<int32_t>();
   }
+  P.vtab = nullptr;
+  if (s->engine != kEngineChain && step_layout(n, D, r, Q, m).vcols) {
+    std::vector<int32_t> vt;
+    vphase_cols_tables(I0, n, D, r, Q, m, vt);
+    HIPCHK(s->vtab.alloc(sizeof(int32_t) * vt.size()));
+    HIPCHK(hipMemcpy(s->vtab.p, vt.data(), sizeof(int32_t) * vt.size(), hipMemcpyHostToDevice));
+    P.vtab = s->vtab.as<int32_t>();
+  }
   P.stamps = nullptr;
   P.tline = nullptr;
   P.rms = 0; P.rms_eps = 0.0; P.rms_alpha = 0.0;
   P.wonly = (store_flags & 16) ? 1 : 0;
   P.ncls = (store_flags & 32) ? nchains : 0;
+  P.split = s->engine == kEngineSplit ? split_factor(nchains, D, m, device_cus()) : 1;
   HIPCHK(s->tbase.alloc(sizeof(long long)));
   HIPCHK(hipMemset(s->tbase.p, 0, sizeof(long long)));
   HIPCHK(s->status.alloc(sizeof(int32_t) * nchains));
@@ -417,12 +456,13 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
                b_ord = up(4 * 2 * (size_t)N),
                b_ws = s->store ? up(8 * (size_t)Q * s->nstore) : 0,
                b_Us = s->store ? up(8 * (size_t)n * r * D * s->nstore) : 0,
-               b_dg = s->diag ? up(8 * (size_t)(1 + D) * s->total_steps) : 0;
+               b_dg = s->diag ? up(8 * (size_t)(1 + D) * s->total_steps) : 0,
+               b_sp = P.split > 1 ? up(8 * (size_t)D * P.split * n * r) + up(8 * (size_t)D) : 0;
   std::vector<double> w0(Q), U0((size_t)n * r * D);
   s->chains_h.resize(nchains);
   for (int c = 0; c < nchains; ++c) {
     std::unique_ptr<DevMem> mem(new DevMem());
-    HIPCHK(mem->alloc(b_w + b_U + b_temp + b_ord + b_ws + b_Us + b_dg));
+    HIPCHK(mem->alloc(b_w + b_U + b_temp + b_ord + b_ws + b_Us + b_dg + b_sp));
     char* base = mem->as<char>();
     ChainDesc& C = s->chains_h[c];
     C.phi = phi_dev[c];
@@ -437,6 +477,14 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     C.status = s->status.as<int32_t>() + c;
     C.seed = seeds[c];
     C.gw = C.gU = C.res = nullptr;
+    C.gpart = nullptr;
+    C.gcnt = nullptr;
+    if (b_sp) {
+      char* sp = base + b_w + b_U + b_temp + b_ord + b_ws + b_Us + b_dg;
+      C.gpart = (double*)sp;
+      C.gcnt = (unsigned long long*)(sp + up(8 * (size_t)D * P.split * n * r));
+      HIPCHK(hipMemset(C.gcnt, 0, 8 * (size_t)D));
+    }
     C.epsw = cfg->epsw; C.epsU = cfg->epsU; C.signal_var = cfg->signal_var; C.sigma_w = cfg->sigma_w;
     host_init_state(n, r, D, Q, seeds[c], cfg->stiefel != 0, cfg->sigma_w, w0.data(), U0.data());
     HIPCHK(hipMemcpy(C.w, w0.data(), 8 * (size_t)Q, hipMemcpyHostToDevice));
@@ -669,7 +717,8 @@ extern "C" int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int6
     const int rc = session_prime(s);
     if (rc != GPT_OK) return rc;
   }
-  const size_t per = (size_t)(s->P.D + 1) * s->nchains * kStamps;
+  // one slot row per workgroup of a step: D+1 per chain, D·S+1 under the split engine
+  const size_t per = (size_t)(s->P.D * std::max(1, s->P.split) + 1) * s->nchains * kStamps;
   DevMem buf;
   HIPCHK(buf.alloc(8 * per * cnt));
   HIPCHK(hipMemset(buf.p, 0, 8 * per * cnt));
@@ -741,7 +790,7 @@ extern "C" int gpt_sgld_session_info(gpt_sgld_session* s, int64_t* out) {
   } else {
     out[1] = (int64_t)step_layout(P.n, P.D, P.r, P.Q, P.m).bytes;
     out[2] = kNT;
-    out[3] = (int64_t)(P.D + 1) * s->nchains;
+    out[3] = (int64_t)(P.D * (P.split > 1 ? P.split : 1) + 1) * s->nchains;
   }
   return GPT_OK;
 }
@@ -859,6 +908,10 @@ static int host_sampler(const gpt_sgld_config* cfg, const double* phi, const dou
   int32_t st = 0;
   rc = gpt_sgld_session_fetch(s, 0, w_store, U_store, diag, &st);
   if (rc != GPT_OK) return rc;
+  if (st == 2) {                             // split engine: an in-kernel barrier timed out
+    set_error("split engine: the batch-slice barrier timed out (grid not resident)");
+    return GPT_ERR_HIP;
+  }
   if (st) {
     set_error("Get NaN when moving along Geodesic. Try smaller epsU");
     return GPT_ERR_NAN_GEODESIC;

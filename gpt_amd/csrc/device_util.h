@@ -308,6 +308,71 @@ __device__ __forceinline__ void vphase_tile(const double* temp_l, int MP, const 
   }
 }
 
+// The V-phase of vphase_tile in the column-lane form (the step kernel's latency path): lanes =
+// batch columns i = c0 + lane, waves = contiguous slices of the core entries q.  q is wave-uniform,
+// so every temp read is one contiguous 512-B row segment (no gather, no transpose-reduce), and
+// the LDS table entry of q (vphase_cols_tables, 16 ints) is three broadcast reads: the 8 temp row offsets
+// of its factors — the D−1 factors k ≠ kown in k order, ones-row padding, the kown factor last —
+// and I[q, kown].  val[1+l] gets the leave-one-out product, val[0] = that product · temp[kown]
+// (the w block's table has all D factors in k order).  Four entries per pass keep 32 LDS reads
+// in flight.  The per-wave partial sums (NC per column) meet in vred (kNW·NC·64 doubles) and are
+// summed in wave order.
+template <int R, bool WITHA, class Out>
+__device__ __forceinline__ void vphase_cols(const double* temp_l, const int32_t* tab,
+                                            const double* w_l, int Q, int Bt, double* vred,
+                                            Out out) {
+  constexpr int NC = WITHA ? 1 + R : 1;
+  constexpr int QU = 4;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+  const int Qw = (Q + kNW - 1) / kNW;
+  const int qa = wv * Qw, qb = min(Q, qa + Qw);
+  for (int c0 = 0; c0 < Bt; c0 += 64) {
+    const double* tcol = temp_l + min(c0 + lane, Bt - 1);
+    double f = 0.0, a[R];
+#pragma unroll
+    for (int l = 0; l < R; ++l) a[l] = 0.0;
+    for (int q0 = qa; q0 < qb; q0 += QU) {
+      double vk[QU], t7[QU], wq[QU];
+      int lk[QU];
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        const int q = min(q0 + u, qb - 1);             // past the slice: weight 0
+        const int4 e0 = *(const int4*)(tab + 16 * q), e1 = *(const int4*)(tab + 16 * q + 4);
+        wq[u] = q0 + u < qb ? w_l[q] : 0.0;
+        const double t0 = tcol[e0.x], t1 = tcol[e0.y], t2 = tcol[e0.z], t3 = tcol[e0.w];
+        const double t4 = tcol[e1.x], t5 = tcol[e1.y], t6 = tcol[e1.z];
+        t7[u] = tcol[e1.w];
+        vk[u] = ((((((t0 * t1) * t2) * t3) * t4) * t5) * t6);
+        lk[u] = WITHA ? uni(tab[16 * q + 8]) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < QU; ++u) {
+        f = fma(wq[u], vk[u] * t7[u], f);
+        if (WITHA) {
+          const double cc = wq[u] * vk[u];
+#pragma unroll
+          for (int l = 0; l < R; ++l)
+            if (l == lk[u]) a[l] += cc;
+        }
+      }
+    }
+    vred[wv * NC * 64 + lane] = f;
+    if (WITHA) {
+#pragma unroll
+      for (int l = 0; l < R; ++l) vred[(wv * NC + 1 + l) * 64 + lane] = a[l];
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < NC * 64; o += kNT) {
+      const int comp = o >> 6, ln = o & 63;
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < kNW; ++w) s += vred[(w * NC + comp) * 64 + ln];
+      if (c0 + ln < Bt) out(comp, c0 + ln, s);
+    }
+    __syncthreads();
+  }
+}
+
 // Gram products over j < n of LDS rows (stride NP), lanes = outputs, waves = j slices.
 //  mode 0: out[a*R+b] = Σ_j X[a][j]·Y[b][j]                      (R² outputs)
 //  mode 1: out[a*R+b] = Σ X[a]Y[b];  out[R²+a*R+b] = Σ Y[a]Y[b]   (2R² outputs)

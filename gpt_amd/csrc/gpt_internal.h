@@ -21,6 +21,8 @@ constexpr int kNW = kNT / 64;      // waves per workgroup
 constexpr int kDMax = 16;          // max input dimensions D handled by the kernels
 constexpr int kEngineGrid = 0;     // sgld.hip: grid (D+1, chains), two batch reads per step
 constexpr int kEngineChain = 1;    // chain.hip: one workgroup per chain, one batch read per step
+constexpr int kEngineSplit = 2;    // sgld.hip with P.split = S: grid (D·S + 1, chains), the batch
+                                   // in S slices per dimension (single-chain latency)
 
 // Per-chain device state.  All pointers are device pointers.
 struct ChainDesc {
@@ -40,6 +42,9 @@ struct ChainDesc {
   double* gw;            // RMSprop (GPT_SGLD.jl:1121): Q moving average of squared gradw
   double* gU;            //   n*r*D moving average of squared gradU
   double* res;           //   m residuals of the step (written by the w phase)
+  double* gpart;         // split engine: D·S partial gradU (n·r each, unscaled) of the batch
+                         //   slices, [(k·S + s)·r + l]·n + j
+  unsigned long long* gcnt;   // split engine: D arrival counters (S per step, never reset)
 };
 
 struct StepParams {
@@ -51,12 +56,17 @@ struct StepParams {
   const int32_t* I0;              // Q*D 0-based, layout q + Q*k
   const int32_t* runq;            // chain engine: runq[(k*r + l)*64 + s] = s-th q (ascending) with
                                   // I[q,k] = l, or 256 (a zero slot) past the run's end
+  const int32_t* vtab;            // grid engine, column-lane V-phase: per workgroup kind (k < D,
+                                  // w block = D) and core entry q, 16 ints: 8 temp row offsets
+                                  // and I[q, k] (vphase_cols_tables), or null (vphase_tile)
   long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
   long long* tline;               // chain engine: per-workgroup timeline (kTimeline per block) or null
   int rms;                        // 1: GPT_SGLDERM_RMSprop steps (grid engine, two launches)
   int wonly;                      // 1: GPT_SGLDERMw steps (w alone, U fixed; grid engine)
   int ncls;                       // >= 2: GPTclassification, chains are the classes of one
                                   // model (grid engine; ChainDesc.res = class fhat, .gU = gradU)
+  int split;                      // grid engine: S >= 2 workgroups per dimension, each on one
+                                  // slice of the minibatch (the split engine, kEngineSplit), else 1
   double rms_eps, rms_alpha;      // its epsilon and moving-average coefficient
 };
 constexpr int kStamps = 16;       // stamp slots per block
@@ -73,9 +83,9 @@ GPT_HD size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
 //   expm    : W_l | expm0 (7·(2R)²) | expm1 (7·R²)       (U_l/redG dead; old U re-read from HBM)
 //   update  : W_l | U_l | redG                           (new U; P5 reads U_l)
 struct StepLayout {
-  int MP, NP, NS, conc, keepU;    // NP: n padded to 64 (loop range), NS = NP+1 row stride
+  int MP, NP, NS, conc, keepU, vcols;   // NP: n padded to 64 (loop range), NS = NP+1 row stride
   size_t o_I, o_w, o_idx, o_y, o_res, o_coef, o_gram, o_Ec, o_mx, o_un;
-  size_t o_temp, o_W, o_U, o_red, o_x0, o_x1, bytes;
+  size_t o_temp, o_W, o_U, o_red, o_x0, o_x1, o_ones, o_vred, o_vtab, bytes;
 };
 
 GPT_HD StepLayout step_layout(int n, int D, int r, int Q, int m) {
@@ -119,6 +129,15 @@ GPT_HD StepLayout step_layout(int n, int D, int r, int Q, int m) {
     const size_t ux = L.conc ? nrp + x0 + x1 : nrp + x0;
     if (ux > un) un = ux;
   }
+  // the column-lane V-phase (vphase_cols, D <= 8) keeps after temp_l a row of MP ones, its
+  // per-wave partial sums (kNW·(1+r)·64 doubles) and its table (16 ints per q), when that still
+  // fits the LDS; otherwise the step uses vphase_tile
+  L.o_ones = o + al16(un_v);
+  L.o_vred = L.o_ones + al16(8 * (size_t)L.MP);
+  L.o_vtab = L.o_vred + 8 * (size_t)kNW * (1 + r) * 64;
+  const size_t vend = L.o_vtab + 64 * (size_t)Q - o;
+  if (D <= 8 && vend > un && al16(o + vend) <= cap) un = vend;
+  L.vcols = (D <= 8 && vend <= un) ? 1 : 0;
   L.bytes = al16(o + un);
   return L;
 }
@@ -163,6 +182,9 @@ hipError_t launch_epoch_order(const ChainDesc* chains, int nchains, int N, int n
                               long long total_steps, const long long* tbase, int t_local,
                               int e_fixed, int32_t* ws, hipStream_t st);
 bool rank_supported(int r);
+// vphase_cols' tables for a session (step_layout(n, D, r, Q, m).vcols): (D+1)·Q·16 ints
+void vphase_cols_tables(const std::vector<int32_t>& I0, int n, int D, int r, int Q, int m,
+                        std::vector<int32_t>& out);
 
 // Chain-resident engine (chain.hip): one workgroup per chain, many steps per launch.
 bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stiefel,

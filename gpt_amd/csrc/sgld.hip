@@ -27,6 +27,9 @@ namespace gpt {
 #ifndef GPT_TOUCH
 #define GPT_TOUCH 1       // L2 touch of the next batch's rows during the V-phase
 #endif
+#ifndef VPHASE_COLS
+#define VPHASE_COLS 1     // the column-lane V-phase (vphase_cols) where the LDS has its scratch
+#endif
 constexpr int kTouch = 4;   // row pairs per wave: 2·kNW·kTouch = 64 rows >= the minibatch
 
 template <int R>
@@ -37,8 +40,13 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const ChainDesc C = chains[blockIdx.y];
   // kbase = D: the RMSprop w phase (one workgroup); kbase = D + 1: the class-fhat pass of
-  // GPTclassification (one workgroup per class, before the step launch)
-  const int k = blockIdx.x + kbase;
+  // GPTclassification (one workgroup per class, before the step launch).
+  // Split engine (P.split = S >= 2, kbase = 0): workgroup x < D·S is (k = x / S, slice x % S) of
+  // the minibatch; x = D·S is the w block.
+  const int S = (P.split > 1 && kbase == 0) ? P.split : 1;
+  const int k = S > 1 ? ((int)blockIdx.x < P.D * S ? (int)blockIdx.x / S : P.D)
+                      : (int)blockIdx.x + kbase;
+  const int sl = (S > 1 && k < P.D) ? (int)blockIdx.x - k * S : 0;
   const int tid = threadIdx.x, wv = uni(tid >> 6);
   const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
@@ -47,6 +55,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   const int n = P.n, D = P.D, Q = P.Q, m = P.m;
   const StepLayout L = step_layout(n, D, R, Q, m);
   const int MP = L.MP, NP = L.NP, NS = L.NS;
+  const bool vcols = VPHASE_COLS && P.vtab && k <= D;   // not the class-fhat pass (k = D + 1)
   int* IT_l = (int*)(smem + L.o_I);            // I transposed: kk*Q + q
   double* w_l = (double*)(smem + L.o_w);
   int* idx_l = (int*)(smem + L.o_idx);
@@ -72,37 +81,50 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   const bool has_next = t1 < P.total_steps;
   const int B1 = has_next ? min(m, P.N - s1) : 0;
   const int32_t* ord1 = C.order + (size_t)((has_next ? e1 : e) & 1) * P.N + (has_next ? s1 : start);
+  // this workgroup's batch columns [r0, r0 + Bs) and next-batch columns [r0n, r0n + Bsn)
+  const bool sliced = S > 1 && k < D;
+  const int r0 = sliced ? (Bt * sl) / S : 0;
+  const int Bs = sliced ? (Bt * (sl + 1)) / S - r0 : Bt;
+  const int r0n = sliced ? (B1 * sl) / S : 0;
+  const int Bsn = sliced ? (B1 * (sl + 1)) / S - r0n : B1;
   // rows of the next batch this lane touches into L2 during the V-phase (P5 streams them at the
   // end of the step): lanes 0-31 / 32-63 of wave w cover rows 2(w + kNW·x) + {0, 1}
   int trow[kTouch];
-  const bool touch = GPT_TOUCH && k < D && has_next;
+  const bool touch = GPT_TOUCH && k < D && has_next && Bsn > 0;
   if (touch) {
 #pragma unroll
     for (int x = 0; x < kTouch; ++x) {
       const int i = 2 * (wv + kNW * x) + ((tid & 63) >> 5);
-      trow[x] = gptr(ord1)[min(i, B1 - 1)];      // past the batch: its last row again
+      trow[x] = gptr(ord1)[r0n + min(i, Bsn - 1)];   // past the slice: its last row again
     }
   }
   STAMP(0);
 
   // ---- P0: stage temp (this batch), I, w, batch rows and targets
   {
-    const double* tsrc = C.temp + (size_t)(t & 1) * D * R * m;
-    for (int o = tid; o < D * R * MP; o += kNT) {   // zero tail: unrolled reads run past Bt
+    const double* tsrc = C.temp + (size_t)(t & 1) * D * R * m + r0;
+    for (int o = tid; o < D * R * MP; o += kNT) {   // zero tail: unrolled reads run past Bs
       const int row = o / MP, i = o - row * MP;
-      temp_l[o] = i < Bt ? gptr(tsrc)[row * m + i] : 0.0;
+      temp_l[o] = i < Bs ? gptr(tsrc)[row * m + i] : 0.0;
     }
     for (int i = tid; i < MP; i += kNT) res_l[i] = 0.0;
     for (int o = tid; o < Q * D; o += kNT) IT_l[o] = gptr(P.I0)[o];   // I0 is already q + Q*k
     // RMSprop U phase: A uses the new w written by the w phase (GPT_SGLD.jl:1193-1199)
     const double* wsrc = C.w + (size_t)(((P.rms && k < D) ? t + 1 : t) & 1) * Q;
     for (int q = tid; q < Q; q += kNT) w_l[q] = gptr(wsrc)[q];
-    for (int i = tid; i < Bt; i += kNT) {
-      const int row = gptr(ord)[i];
+    for (int i = tid; i < Bs; i += kNT) {
+      const int row = gptr(ord)[r0 + i];
       idx_l[i] = row;
       y_l[i] = gptr(C.y)[row];
     }
     for (int o = tid; o < R * MP; o += kNT) coef_l[o] = 0.0;
+    if (vcols) {
+      double* ones = (double*)(smem + L.o_ones);
+      for (int i = tid; i < MP; i += kNT) ones[i] = 1.0;
+      const int4* tg = (const int4*)(P.vtab + (size_t)k * Q * 16);
+      int4* tl = (int4*)(smem + L.o_vtab);
+      for (int o = tid; o < 4 * Q; o += kNT) tl[o] = tg[o];
+    }
   }
   __syncthreads();
   STAMP(1);
@@ -126,10 +148,15 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       if (comp == 0) res_l[i] = P.ncls ? v : y_l[i] - v;      // classification: fhat itself
       else coef_l[(comp - 1) * MP + i] = v;
     };
-    if (Bt <= kNW * VCfg<R>::ICV_SMALL)
-      vphase_tile<R, VCfg<R>::ICV_SMALL>(temp_l, MP, IT_l, w_l, Q, D, k >= D ? 0 : k, Bt, vout);
+    if (vcols) {
+      double* vred = (double*)(smem + L.o_vred);
+      const int32_t* tab = (const int32_t*)(smem + L.o_vtab);
+      if (k < D) vphase_cols<R, true>(temp_l, tab, w_l, Q, Bs, vred, vout);
+      else vphase_cols<R, false>(temp_l, tab, w_l, Q, Bs, vred, vout);
+    } else if (Bs <= kNW * VCfg<R>::ICV_SMALL)
+      vphase_tile<R, VCfg<R>::ICV_SMALL>(temp_l, MP, IT_l, w_l, Q, D, k >= D ? 0 : k, Bs, vout);
     else
-      vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, IT_l, w_l, Q, D, k >= D ? 0 : k, Bt, vout);
+      vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, IT_l, w_l, Q, D, k >= D ? 0 : k, Bs, vout);
   }
   if (touch) {
 #pragma unroll
@@ -256,8 +283,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     __syncthreads();
   }
   // coef[l][i] = A[l][i]·res[i]; stage U^(k) (the union slot of temp_l is free now)
-  for (int o = tid; o < R * Bt; o += kNT) {
-    const int l = o / Bt, i = o - l * Bt;
+  for (int o = tid; o < R * Bs; o += kNT) {
+    const int l = o / Bs, i = o - l * Bs;
     coef_l[l * MP + i] *= res_l[i];
   }
   const double* Ug = C.U + (size_t)n * R * k;
@@ -292,27 +319,9 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   double gn2 = 0.0, esum = 0.0;
   // Uniform trip count (j clamped, writes masked): every lane takes part in the row-vector
   // load below, so v_readlane never reads a lane that skipped it.
-  for (int j0 = 0; j0 < n; j0 += kNT) {
-    const int j = j0 + tid;
-    const bool jok = j < n;
-    const int jc = jok ? j : n - 1;
-    double acc[R];
-#pragma unroll
-    for (int l = 0; l < R; ++l) acc[l] = 0.0;
-    for (int i0 = 0; i0 < Bt; i0 += 32) {
-      const int vrow = batch_rows_lane(ord, 0, i0, Bt);      // lane u: row of column i0+u
-      double p[32];
-#pragma unroll
-      for (int u = 0; u < 32; ++u) {
-        const int row = __builtin_amdgcn_readlane(vrow, u);  // columns past Bt: clamped row
-        p[u] = (gptr(C.phi) + koff + (long long)row * rstride)[jc];
-      }
-#pragma unroll
-      for (int u = 0; u < 32; ++u)
-#pragma unroll
-        for (int l = 0; l < R; ++l) acc[l] = fma(p[u], coef_l[l * MP + i0 + u], acc[l]);
-    }
-    if (jok && P.rms) {           // :1212-1227: ĝU, moving average, N·ĝU kept until εU_k is known
+  // the drive of row j from its gradient sums acc[l] = Σ_i phi[j,k,i]·A[l,k,i]·res_i
+  auto drive = [&](int j, const double (&acc)[R]) {
+    if (P.rms) {                  // :1212-1227: ĝU, moving average, N·ĝU kept until εU_k is known
 #pragma unroll
       for (int l = 0; l < R; ++l) {
         const double gr = acc[l] / ((double)Bt * C.signal_var);
@@ -324,7 +333,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
         gn2 = fma(G, G, gn2);
         W_l[l * NS + j] = G;
       }
-    } else if (jok) {
+    } else {
 #pragma unroll
       for (int l = 0; l < R; ++l) {
         const double G = acc[l] * cU;
@@ -337,6 +346,78 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
           U_l[l * NS + j] = u + (C.epsU * (G - n * u) / 2 + sq * W_l[l * NS + j]);
         }
       }
+    }
+  };
+  for (int j0 = 0; j0 < n; j0 += kNT) {
+    const int j = j0 + tid;
+    const bool jok = j < n;
+    const int jc = jok ? j : n - 1;
+    double acc[R];
+#pragma unroll
+    for (int l = 0; l < R; ++l) acc[l] = 0.0;
+    for (int i0 = 0; i0 < Bs; i0 += 32) {
+      const int vrow = batch_rows_lane(ord + r0, 0, i0, Bs);  // lane u: row of column i0+u
+      double p[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int row = __builtin_amdgcn_readlane(vrow, u);  // columns past Bs: clamped row
+        p[u] = (gptr(C.phi) + koff + (long long)row * rstride)[jc];
+      }
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+#pragma unroll
+        for (int l = 0; l < R; ++l) acc[l] = fma(p[u], coef_l[l * MP + i0 + u], acc[l]);
+    }
+    if (S > 1) {                  // the slice's partial sums; summed over the slices below
+      if (jok) {
+#pragma unroll
+        for (int l = 0; l < R; ++l)   // agent-coherent store: written through this XCD's L2
+          __hip_atomic_store(C.gpart + ((size_t)(k * S + sl) * R + l) * n + j, acc[l],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
+    if (jok) drive(j, acc);
+  }
+  if (S > 1) {
+    // the S workgroups of dimension k meet here (all of the grid is resident: the engine is only
+    // chosen when D·S + 1 workgroups per chain fit the GPU at once); each then sums the S partial
+    // sums in slice order — the same doubles in every one of them — and runs the rest of the step
+    // redundantly (the same noise, the same Stiefel move), so no second launch is needed.
+    // The slices of one dimension sit on different XCDs (L2s).  The exchange uses agent-scope
+    // relaxed atomics for the partial sums, the counter and its polls — each access goes to the
+    // coherence point on its own — and orders them by waiting for the stores' completion
+    // (s_waitcnt) before the arrival: agent-scope release/acquire FENCES would instead write back
+    // and invalidate the whole L2 of the XCD (every poll), evicting the next batch's rows.
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long* cnt = C.gcnt + k;
+      __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long target = (unsigned long long)S * (unsigned long long)(t + 1);
+      long long spins = 0;
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1ll << 26)) {             // never expected: a barrier that cannot close
+          __hip_atomic_store(C.status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    for (int j0 = 0; j0 < n; j0 += kNT) {
+      const int j = j0 + tid;
+      if (j >= n) continue;
+      double acc[R];
+#pragma unroll
+      for (int l = 0; l < R; ++l) {
+        double a = 0.0;
+        for (int s2 = 0; s2 < S; ++s2)
+          a += __hip_atomic_load(C.gpart + ((size_t)(k * S + s2) * R + l) * n + j,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[l] = a;
+      }
+      drive(j, acc);
     }
   }
   if (C.diag) {
@@ -492,7 +573,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   {
     double* Uk = C.U + (size_t)n * R * k;
     double* Us = (store && C.U_store) ? C.U_store + ((size_t)slot * D + k) * n * R : nullptr;
-    for (int o = tid; o < R * n; o += kNT) {
+    for (int o = tid; o < (sl == 0 ? R * n : 0); o += kNT) {   // split: slice 0 writes
       const int l = o / n, j = o - l * n;
       const double u = U_l[l * NS + j];
       gptr_w(Uk)[o] = u;
@@ -504,8 +585,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   if (has_next) {
     __syncthreads();
     STAMP(9);
-    double* tdst = C.temp + (size_t)(t1 & 1) * D * R * m + (size_t)k * R * m;
-    phidotU_tile<R>(C.phi, koff, rstride, ord1, 0, B1, n, NP, NS, U_l,
+    double* tdst = C.temp + (size_t)(t1 & 1) * D * R * m + (size_t)k * R * m + r0n;
+    phidotU_tile<R>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS, U_l,
                     [&](int l, int i, double v) { gptr_w(tdst)[l * m + i] = v; });
     __syncthreads();
     STAMP(10);
@@ -548,6 +629,25 @@ __global__ void advance_kernel(long long* tbase, long long by) {
 
 #define GPT_RANKS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(15) X(16) X(20)
 
+void vphase_cols_tables(const std::vector<int32_t>& I0, int n, int D, int r, int Q, int m,
+                        std::vector<int32_t>& out) {
+  const StepLayout L = step_layout(n, D, r, Q, m);
+  const int ones = (int)((L.o_ones - L.o_temp) / 8), MP = L.MP;
+  out.assign((size_t)(D + 1) * Q * 16, 0);
+  for (int k = 0; k <= D; ++k)
+    for (int q = 0; q < Q; ++q) {
+      int32_t* e = out.data() + ((size_t)k * Q + q) * 16;
+      for (int s = 0; s < 8; ++s) {
+        int kk = -1;
+        if (k == D) kk = s < D ? s : -1;                 // w block: all factors in k order
+        else if (s == 7) kk = k;                         // own factor last
+        else if (s < D - 1) kk = s < k ? s : s + 1;      // the others in k order
+        e[s] = kk < 0 ? ones : (kk * r + I0[q + (size_t)Q * kk]) * MP;
+      }
+      e[8] = k < D ? I0[q + (size_t)Q * k] : 0;
+    }
+}
+
 bool rank_supported(int r) {
   switch (r) {
 #define CASE(RR) case RR:
@@ -577,7 +677,7 @@ hipError_t launch_temp_init(const StepParams& P, const ChainDesc* chains, int nc
 hipError_t launch_step(const StepParams& P, const ChainDesc* chains, int nchains,
                        const long long* tbase, int t_local, hipStream_t st) {
   const StepLayout L = step_layout(P.n, P.D, P.r, P.Q, P.m);
-  dim3 grid(P.D + 1, nchains);
+  dim3 grid(P.D * (P.split > 1 ? P.split : 1) + 1, nchains);
   switch (P.r) {
 #define CASE(RR)                                                                              \
   case RR:                                                                                    \

@@ -15,8 +15,8 @@ from .GPT_SGLD import make_config
 
 
 # store_flags bits selecting the step engine (include/gptsgld.h, gpt_sgld_session_info)
-ENGINES = {"auto": 0, "grid": 4, "chain": 8}
-ENGINE_NAMES = {0: "grid", 1: "chain"}
+ENGINES = {"auto": 0, "grid": 4, "chain": 8, "split": 64}
+ENGINE_NAMES = {0: "grid", 1: "chain", 2: "split"}
 
 
 class SGLDSession:

@@ -148,7 +148,8 @@ int64_t gpt_sgld_session_steps_done(gpt_sgld_session* s);
  * *avg_us = mean step-kernel duration (the roofline's per-launch time).  Synchronises. */
 int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, double* avg_us);
 /* Diagnostic: run nsteps un-captured steps recording s_memtime (shader-clock ticks)
- * stamps per phase; out = nsteps x (D+1)*nchains x 16 int64 (0 = phase not reached). */
+ * stamps per phase; out = nsteps x W x 16 int64 (0 = phase not reached), W = the workgroups of
+ * one step ((D+1)*nchains; (D*S+1)*nchains under the split engine, gpt_sgld_session_info). */
 int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out);
 /* Diagnostic (chain engine): ONE launch of nsteps steps (within the current epoch, <= 512);
  * out = nchains x gpt_sgld_timeline_slots() int64: per block {s_memrealtime, s_memtime} at slot
@@ -164,9 +165,12 @@ void gpt_sgld_session_destroy(gpt_sgld_session* s);
 /* out[4] = {engine (0 grid: D+1 workgroups per chain, 1 chain: one workgroup per chain),
  *           LDS bytes per workgroup, threads per workgroup, workgroups per step launch}.
  * store_flags of gpt_sgld_session_create: bit0 stores, bit1 diagnostics, bit2 force the grid
- * engine, bit3 force the chain engine (default: the grid engine while nchains*(D+1) workgroups
- * fit the GPU's CUs — the shorter step — else the chain engine whenever the shape allows it;
- * the environment variable GPTSGLD_ENGINE=grid|chain overrides the default). */
+ * engine, bit3 force the chain engine, bit6 force the split engine (engine 2: the grid engine
+ * with the minibatch in S >= 2 slices per dimension, D*S + 1 workgroups per chain, one in-kernel
+ * barrier per step).  Default: the split engine while nchains*(D*S+1) workgroups fit the GPU's
+ * CUs for some S >= 2 (the shortest step), else the grid engine while nchains*(D+1) do, else the
+ * chain engine whenever the shape allows it; GPTSGLD_ENGINE=grid|chain|split overrides the
+ * default and GPTSGLD_SPLIT=S the slice count. */
 int gpt_sgld_session_info(gpt_sgld_session* s, int64_t* out);
 
 /* ---- prediction ---------------------------------------------------------------------- */

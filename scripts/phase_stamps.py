@@ -15,7 +15,7 @@ sys.path.insert(0, ROOT)
 
 CHAIN_NAMES = {1: "prologue (tables, U, rows)", 2: "batch loop", 3: "w update",
                4: "U noise + drive", 5: "proj + geod grams", 6: "expm x2", 7: "tmpU, norm, U write"}
-NAMES = {1: "P0 stage", 2: "P1 V-phase", 3: "w-block gradw / U stage", 4: "P2 gradU+noise",
+NAMES = {1: "P0 stage", 2: "P1 V-phase", 3: "w-block gradw / U stage", 4: "P2 gradU (+barrier)",
          5: "proj gram+mom", 6: "geod grams", 7: "expm x2", 8: "tmpU+norm", 9: "U write+idx",
          10: "P5 next temp"}
 
@@ -29,7 +29,8 @@ def main():
     ap.add_argument("--m", type=int, default=50)
     ap.add_argument("--sgd", action="store_true", help="langevin=False (no noise draws)")
     ap.add_argument("--N", type=int, default=10000, help="training rows used (phi footprint)")
-    ap.add_argument("--engine", default="grid", choices=["grid", "chain"])
+    ap.add_argument("--engine", default="grid", choices=["grid", "chain", "split"])
+    ap.add_argument("--split", type=int, default=2, help="split engine: batch slices S")
     args = ap.parse_args()
     import torch
     import bench
@@ -46,6 +47,8 @@ def main():
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     phi = feature_device(tt(Xtr.T), tt(ls), 1.042, math.sqrt(n / Q ** (1 / D)), tt(Z.T), tt(b.T))
     y = tt(ytr)
+    if args.engine == "split":
+        os.environ["GPTSGLD_SPLIT"] = str(args.split)
     s = SGLDSession(phi, y, I, r, Q, m, 1e-5, 1e-8, 0.0476, 0, 3, list(range(1, args.chains + 1)),
                     store=False, langevin=not args.sgd, engine=args.engine)
     s.run(50)
@@ -110,11 +113,12 @@ def main():
                       % ((nm,) + tuple(dx) + (dict(zip(degs.tolist(), cnt.tolist())),)))
         print("event-timed step kernel: %.2f us" % s.time_steps(20))
         return
-    nb = (D + 1) * args.chains
+    KB = D * (args.split if args.engine == "split" else 1)     # k-blocks per chain
+    nb = (KB + 1) * args.chains
     out = np.zeros((args.steps, nb, 16), dtype=np.int64)
     check(lib().gpt_sgld_session_stamps(s._h, args.steps, out.ctypes.data_as(C.POINTER(C.c_int64))))
-    kblocks = out.reshape(args.steps, args.chains, D + 1, 16)[:, :, :D, :]
-    wblocks = out.reshape(args.steps, args.chains, D + 1, 16)[:, :, D, :]
+    kblocks = out.reshape(args.steps, args.chains, KB + 1, 16)[:, :, :KB, :]
+    wblocks = out.reshape(args.steps, args.chains, KB + 1, 16)[:, :, KB, :]
     print("k-blocks: median cycles per phase (stamp[i] - stamp[i-1])")
     prev = 0
     tot = np.median((kblocks[..., 10] - kblocks[..., 0]).ravel())

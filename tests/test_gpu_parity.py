@@ -202,8 +202,15 @@ def _shape(name):
     return [CASES[name][i] for i in (0, 1, 3, 9, 10)]
 
 
-ENGINE_CASES = [(name, eng) for name in CASES for eng in ("grid", "chain")
-                if eng == "grid" or _chain_ok(*_shape(name))]
+def _split_ok(name):
+    """The split engine takes a batch of >= 12 rows (two slices of 6) and any shape the grid
+    engine takes."""
+    return CASES[name][5] >= 12
+
+
+ENGINE_CASES = [(name, eng) for name in CASES for eng in ("grid", "chain", "split")
+                if eng == "grid" or (eng == "chain" and _chain_ok(*_shape(name)))
+                or (eng == "split" and _split_ok(name))]
 
 
 @pytest.mark.parametrize("name,engine", ENGINE_CASES)
@@ -474,7 +481,7 @@ def test_gpnt_sgld_matches_oracle():
     assert rel(got, want) < 1e-9
 
 
-@pytest.mark.parametrize("engine", ["grid", "chain"])
+@pytest.mark.parametrize("engine", ["grid", "chain", "split"])
 def test_multichain_session_equals_single_runs(engine):
     import torch
     from gpt_amd.session import SGLDSession
@@ -512,6 +519,49 @@ def test_epoch_order_ring_over_many_epochs(engine):
                                    store_every=2)
     assert info["status"] == 0
     assert rel(got_w, wo) < 1e-8 and rel(got_U, Uo) < 1e-8
+
+
+@pytest.mark.parametrize("name,S", [("last_row_alone", 4), ("small", 8), ("ragged_thin", 3),
+                                    ("kin40k_shape", 2)])
+def test_split_engine_slices_match_oracle(name, S, monkeypatch):
+    """The split engine with S forced (GPTSGLD_SPLIT): slices of one row, empty slices of a
+    last batch of one row, ragged slices — the same trajectories as the oracle (the partial
+    gradU sums of the slices add up in slice order, a different rounding than one sum)."""
+    monkeypatch.setenv("GPTSGLD_SPLIT", str(S))
+    n, D, N, r, Q, m, burnin, maxepoch, se, lang, stf = CASES[name]
+    p = make_problem(n, D, N, r, Q, seed=11)
+    epsw, epsU, sv, seed = 1e-4, 1e-6, 0.05, 23
+    ws, Us, dg = G().GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
+                                   maxepoch, seed, diag=True, langevin=lang, stiefel=stf,
+                                   store_every=se, engine="split")
+    wo, Uo, info = R.GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
+                                   maxepoch, seed, record=True, langevin=lang, stiefel=stf,
+                                   store_every=se)
+    assert info["status"] == 0
+    assert rel(ws, wo) < 1e-8, rel(ws, wo)
+    assert rel(Us, Uo) < 1e-8, rel(Us, Uo)
+    assert rel(dg[1:], np.array(info["gradU_norm"]).T) < 1e-9
+
+
+def test_single_chain_default_and_split_opt_in():
+    """One chain at the kin40k shape: the library picks the grid engine (D + 1 workgroups, the
+    shorter step, scripts/single_chain.py); the split engine is opt-in and runs D·S + 1."""
+    import torch
+    from gpt_amd.session import SGLDSession
+    n, D, N, r, Q, m = 500, 8, 200, 5, 200, 50
+    p = make_problem(n, D, N, r, Q, seed=3)
+    dev = torch.device("cuda", 0)
+    phi = torch.from_numpy(np.ascontiguousarray(np.asarray(p["phi"]).transpose(2, 1, 0))).to(dev)
+    y = torch.from_numpy(np.ascontiguousarray(np.asarray(p["y"], dtype=np.float64))).to(dev)
+    s = SGLDSession(phi, y, p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 1, [5])
+    info = s.info()
+    s.close()
+    assert info["engine"] == "grid" and info["workgroups"] == D + 1
+    s = SGLDSession(phi, y, p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 1, [5], engine="split")
+    info = s.info()
+    s.close()
+    assert info["engine"] == "split" and (info["workgroups"] - 1) % D == 0
+    assert info["workgroups"] > D + 1
 
 
 def test_chain_engine_declines_odd_n_past_one_block():
