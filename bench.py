@@ -129,6 +129,50 @@ def cpu_baseline(phi_np, y_np, I, args, seconds):
                                    T, sT, T, dtT))
 
 
+def cpu_pred_baseline(phi_te, w_all, U_all, fh, I, n, D, r, seconds):
+    """CPU side of the stacked-sample prediction (BASELINE.md:34): the C++ restatement of pred
+    (GPT_SGLD.jl:233-243, oracle/cpu) over all test rows for as many of the GPU's samples as fit
+    about seconds/4 on the host's cores, checked against the GPU's fhat of the same samples;
+    reported per sample and extrapolated to the GPU call's sample count."""
+    from oracle import cpu_lib
+    T = _cpu_threads()
+    pt = np.asfortranarray(phi_te.cpu().numpy().transpose(2, 1, 0))     # (n, D, Ntest)
+    Nte, Stot = pt.shape[2], w_all.shape[0]
+    wn, Un = w_all.cpu().numpy(), U_all.cpu().numpy()
+    def sample_args(S):
+        return (np.asfortranarray(wn[:S].T),
+                np.reshape(Un[:S].T, (n, r, D, S), order="F"))
+    w1, U1 = sample_args(1)
+    _, sec1 = cpu_lib.pred(w1, U1, I, pt, threads=T)
+    S = int(max(1, min(Stot, (0.25 * seconds) / max(sec1, 1e-6))))
+    wS, US = sample_args(S)
+    f, secS = cpu_lib.pred(wS, US, I, pt, threads=T)
+    ref = fh[:S].cpu().numpy()
+    return dict(ms_per_sample=1e3 * secS / S, samples_timed=S, Ntest=int(Nte), cores=T,
+                ms_est_for_gpu_call=1e3 * secS / S * Stot, gpu_call_samples=int(Stot),
+                max_rel_diff_vs_gpu=float(np.abs(f - ref).max() / np.abs(ref).max()),
+                sample="oracle/cpu gptcpu_pred (pred of GPT_SGLD.jl:233-243, OpenMP over test "
+                       "rows) on %d of the GPU call's samples x %d test rows, %d cores"
+                       % (S, Nte, T))
+
+
+def cpu_b256_baseline(phi_np, y_np, I, args, seconds):
+    """BASELINE.md:35's minibatch-256 variant of the CPU chain (1 chain, 1 core, ~seconds/6)."""
+    from oracle import cpu_lib
+    N = phi_np.shape[2]
+    nb = -(-N // 256)
+    def run(steps):
+        o = cpu_lib.GPTregression_chains(phi_np, y_np, args.signal_var, I, args.r, args.Q, 256,
+                                         args.epsw, args.epsU, 0, -(-steps // nb), [1000],
+                                         threads=1, store_every=(-(-steps // nb)) * nb,
+                                         max_steps=steps)
+        return o["steps"] / o["seconds"], o["steps"], o["seconds"]
+    probe, _, _ = run(4)
+    sps, st, dt = run(max(4, int(probe * seconds / 6)))
+    return dict(value=sps, unit="SGLD steps/s (1 chain, 1 core, minibatch 256)", steps=st,
+                seconds=dt)
+
+
 def chain_seeds(rank, C):
     """param_seed of chain c on this rank: rank·C + c + 1 — distinct over all ranks and chains
     (kin40kExperiment.jl:68 seeds its chains 1..J)."""
@@ -495,6 +539,9 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:          # host cores of rank 0's box, any N
         phi_np = np.asfortranarray(phi_tr.cpu().numpy().transpose(2, 1, 0))
         cpu = cpu_baseline(phi_np, ytr, I, args, args.cpu_seconds)
+        if cpu is not None and "single_core_steps_per_s" in cpu:      # the C++ restatement ran
+            cpu["pred"] = cpu_pred_baseline(phi_te, w_all, U_all, fh, I, n, D, r, args.cpu_seconds)
+            cpu["minibatch_256"] = cpu_b256_baseline(phi_np, ytr, I, args, args.cpu_seconds)
 
     if rank == 0:
         import types

@@ -572,10 +572,24 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
       const hipError_t ee = hipEventCreate(&ev[i]);
       if (ee != hipSuccess) return ee;
     }
-  // temp of up to ~2 GiB of samples per pass; a pass of several workgroup tiles takes a multiple of
+  // temp of up to ~8 GiB of samples per pass; a pass of several workgroup tiles takes a multiple of
   // 128 / gcd(128, r) samples, so its S·r columns fill whole 128-column tiles (no MFMA padding)
   const size_t per_sample = 8 * (size_t)D * r * (size_t)Ntest;
-  int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)S, ((size_t)2 << 30) / per_sample));
+  int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)S, ((size_t)8 << 30) / per_sample));
+  // the pass buffer comes from the device's default stream-ordered pool; keep what the pool holds
+  // between calls (a release threshold of 0 would unmap and remap the ~GBs of every call)
+  {
+    static std::atomic<uint64_t> kept{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && !(kept.load() & (1ull << (dev & 63)))) {
+      hipMemPool_t pool;
+      if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t thr = ~0ull;
+        if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr) == hipSuccess)
+          kept.fetch_or(1ull << (dev & 63));
+      }
+    }
+  }
   {
     int g = 128, b = r;
     while (b) { const int t = g % b; g = b; b = t; }

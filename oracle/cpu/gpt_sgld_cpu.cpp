@@ -493,6 +493,49 @@ long long gptcpu_regression(const int64_t* icfg, const double* dcfg, const doubl
   return total;
 }
 
+// pred (GPT_SGLD.jl:233-243) for S samples over Ntest rows: fhat[s·Ntest + i] =
+// Σ_q w_s[q]·Π_k temp[k, I[q,k], i], temp = phidotU(U_s, phitest) (:193-205, :208-230), with
+// phitest in the reference layout (n, D, Ntest), w (Q, S), U (n·r·D, S).  OpenMP over test
+// rows; *seconds: wall time.  The CPU side of the stacked-sample prediction (BASELINE.md:34).
+void gptcpu_pred(int64_t n, int64_t D, int64_t Ntest, int64_t r, int64_t Q, int64_t S,
+                 const double* phitest, const double* w, const double* U, const int32_t* I,
+                 int threads, double* fhat, double* seconds) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t nrD = (size_t)n * r * D;
+#ifdef _OPENMP
+  if (threads < 1) threads = omp_get_max_threads();
+#pragma omp parallel num_threads(threads)
+#endif
+  {
+    std::vector<double> temp((size_t)D * r);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+    for (long long i = 0; i < Ntest; ++i)
+      for (int64_t s = 0; s < S; ++s) {
+        const double* Us = U + (size_t)s * nrD;
+        for (int64_t k = 0; k < D; ++k) {
+          const double* pk = phitest + (size_t)n * (k + (size_t)D * i);
+          for (int64_t l = 0; l < r; ++l) {
+            const double* ul = Us + (size_t)n * (l + (size_t)r * k);
+            double a = 0.0;
+#pragma omp simd reduction(+ : a)
+            for (int64_t j = 0; j < n; ++j) a += pk[j] * ul[j];
+            temp[k + (size_t)D * l] = a;
+          }
+        }
+        double f = 0.0;
+        for (int64_t q = 0; q < Q; ++q) {
+          double v = 1.0;
+          for (int64_t k = 0; k < D; ++k) v *= temp[k + (size_t)D * (I[q + (size_t)Q * k] - 1)];
+          f += v * w[q + (size_t)Q * s];
+        }
+        fhat[(size_t)s * Ntest + i] = f;
+      }
+  }
+  *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int gptcpu_max_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

@@ -26,6 +26,9 @@ def lib():
                                         C.c_int, C.POINTER(C.c_uint64), C.c_int, P_D, P_D, P_D, P_D,
                                         C.POINTER(C.c_int32), P_D]
         L.gptcpu_max_threads.restype = C.c_int
+        L.gptcpu_pred.restype = None
+        L.gptcpu_pred.argtypes = [C.c_int64] * 6 + [P_D, P_D, P_D, C.POINTER(C.c_int32), C.c_int,
+                                                    P_D, P_D]
         _LIB = L
     return _LIB
 
@@ -64,6 +67,23 @@ def GPTregression_chains(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, max
     if stores:
         out.update(w_store=ws, U_store=Us)
     return out
+
+
+def pred(w, U, I, phitest, threads=1):
+    """pred (GPT_SGLD.jl:233-243) of S samples: w (Q, S), U (n, r, D, S), phitest (n, D, Ntest)
+    in the reference layouts.  Returns (fhat (S, Ntest), seconds)."""
+    phitest = np.asfortranarray(phitest, dtype=np.float64)
+    n, D, Nt = phitest.shape
+    w = np.asfortranarray(np.asarray(w, dtype=np.float64).reshape(w.shape[0], -1))
+    Q, S = w.shape
+    U = np.asfortranarray(np.asarray(U, dtype=np.float64).reshape(n, -1, D, S))
+    r = U.shape[1]
+    I = np.asfortranarray(I, dtype=np.int32)
+    f = np.zeros((S, Nt))
+    sec = C.c_double(0.0)
+    lib().gptcpu_pred(n, D, Nt, r, Q, S, _p(phitest), _p(w), _p(U), _p(I, C.c_int32), int(threads),
+                      _p(f), C.byref(sec))
+    return f, sec.value
 
 
 def cpu_model():

@@ -54,3 +54,18 @@ def test_cpu_nan_bailout_zero_fills():
     wo, Uo, info = R.GPTregression(phi, y * 1e8, 1e-12, I, 2, 4, 5, 1.0, 1.0, 0, 2, 3)
     assert info["status"] == 1 and got["status"][0] == 1
     assert not got["w_store"].any() and not got["U_store"].any()
+
+
+def test_cpu_pred_matches_oracle():
+    """The CPU prediction baseline (gptcpu_pred) is pred of GPT_SGLD.jl:233-243 per sample."""
+    rng = np.random.default_rng(5)
+    n, D, Nt, r, Q, S = 20, 3, 57, 4, 30, 3
+    phi = np.asfortranarray(rng.standard_normal((n, D, Nt)) * 0.3)
+    w = rng.standard_normal((Q, S))
+    U = rng.standard_normal((n, r, D, S)) * 0.3
+    I = rng.integers(1, r + 1, size=(Q, D)).astype(np.int32)
+    f, sec = cpu.pred(w, U, I, phi, threads=2)
+    for s in range(S):
+        want = R.pred(w[:, s], U[..., s], I, phi)
+        assert np.abs(f[s] - want).max() <= 1e-12 * np.abs(want).max()
+    assert sec >= 0.0
