@@ -52,8 +52,14 @@ namespace gpt {
 #endif
 constexpr int kChainBufs = CHAIN_DBUF ? 2 : 1;
 constexpr int kChainDMax = 8;     // waves per workgroup (one per input dimension)
-constexpr int kChainTasks = 2;    // V-phase tasks per wave (NCH·G <= tasks·D); J = 8: 1
-constexpr int kChainG = 2;        // batch rows per group
+#ifndef CHAIN_G
+#define CHAIN_G 2                 // batch rows per group
+#endif
+#ifndef CHAIN_TPW8
+#define CHAIN_TPW8 1              // V tasks per wave at J = 8, D > 4
+#endif
+constexpr int kChainTasks = 2;    // V-phase tasks per wave (NCH·G <= tasks·D); J = 8: CHAIN_TPW8
+constexpr int kChainG = CHAIN_G;  // batch rows per group
 constexpr int kChainQPL = 4;      // q chunks of 64 (Q <= 64·kChainQPL)
 constexpr int kChainQP = 64 * kChainQPL;
 constexpr int kChainRun = 64;     // members per run (core entries with one value of I[·,k])
@@ -337,7 +343,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 
 
 
-  constexpr int TPW = (J >= 8 && WV > 4) ? 1 : kChainTasks;   // one task per wave at J = 8, D > 4
+  constexpr int TPW = (J >= 8 && WV > 4) ? CHAIN_TPW8 : kChainTasks;   // J = 8, D > 4: one task
   for (;;) {                             // ---------------------------------- one SGLD step
   // thread ids formed inside the step from v_mbcnt (not threadIdx.x): per-lane addresses are not
   // hoisted out of the step loop, and v0 need not be kept — the register-bound kernel used to spill
@@ -903,7 +909,7 @@ bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stie
   if (chain_J(n) >= 2 && (n & 1)) return false;   // 16-B row staging needs 16-B aligned rows
   if (Q > kChainQP || m > kChainMMax) return false;   // the fixed LDS carve's maxima
   const int NT = (Q + 63) / 64 * kChainG;
-  if (NT > ((chain_J(n) >= 8 && D > 4) ? 1 : kChainTasks) * D) return false;
+  if (NT > ((chain_J(n) >= 8 && D > 4) ? CHAIN_TPW8 : kChainTasks) * D) return false;
   return chain_lds_bytes(n, D, r, Q, m) + chain_static_lds(chain_J(n), chain_wv(D)) <= 160 * 1024;
 }
 

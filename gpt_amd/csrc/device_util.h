@@ -198,6 +198,23 @@ __device__ __forceinline__ int batch_rows_lane(const int32_t* ordp, int rowbase,
   return ordp ? gptr(ordp)[i] : rowbase + i;
 }
 
+// Per-lane row addresses base + row·stride of a wave's rows, read back one lane at a time (a
+// uniform lane index) as two v_readlane halves: a scalar address, so the row's load is the
+// saddr + 32-bit lane offset form with no per-row 64-bit address arithmetic.
+struct RowPtr {
+  unsigned lo, hi;
+  __device__ __forceinline__ RowPtr(const double* base, int row, long long stride) {
+    const unsigned long long v = (unsigned long long)(base + (long long)row * stride);
+    lo = (unsigned)v;
+    hi = (unsigned)(v >> 32);
+  }
+  __device__ __forceinline__ const __attribute__((address_space(1))) double* at(int u) const {
+    return (const __attribute__((address_space(1))) double*)(
+        ((unsigned long long)__builtin_amdgcn_readlane(hi, u) << 32) |
+        (unsigned)__builtin_amdgcn_readlane(lo, u));
+  }
+};
+
 template <int R, class Out>
 __device__ __forceinline__ void phidotU_tile(const double* __restrict__ phi, long long koff,
                                              long long rstride, const int32_t* ordp, int rowbase,
@@ -210,13 +227,10 @@ __device__ __forceinline__ void phidotU_tile(const double* __restrict__ phi, lon
     double v[C::NV];
 #pragma unroll
     for (int u = 0; u < C::NV; ++u) v[u] = 0.0;
-    const int vrow = batch_rows_lane(ordp, rowbase, base, Bt);   // kNW·ICH <= 64 columns
+    const RowPtr rp(phi + koff, batch_rows_lane(ordp, rowbase, base, Bt), rstride);   // <= 64 columns
     const __attribute__((address_space(1))) double* rowp[C::ICH];
 #pragma unroll
-    for (int ii = 0; ii < C::ICH; ++ii) {
-      const int c = min(wv + kNW * ii, 63);
-      rowp[ii] = gptr(phi) + koff + (long long)__builtin_amdgcn_readlane(vrow, c) * rstride;
-    }
+    for (int ii = 0; ii < C::ICH; ++ii) rowp[ii] = rp.at(min(wv + kNW * ii, 63));
     const int JS = NP >> 6;
 #pragma unroll 4
     for (int s = 0; s < JS; ++s) {

@@ -30,6 +30,9 @@ namespace gpt {
 #ifndef VPHASE_COLS
 #define VPHASE_COLS 1     // the column-lane V-phase (vphase_cols) where the LDS has its scratch
 #endif
+#ifndef GPT_EXP_P2NOLOAD
+#define GPT_EXP_P2NOLOAD 0   // diagnostics only (wrong results): P2 without its row loads
+#endif
 constexpr int kTouch = 4;   // row pairs per wave: 2·kNW·kTouch = 64 rows >= the minibatch
 
 template <int R>
@@ -356,13 +359,12 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
 #pragma unroll
     for (int l = 0; l < R; ++l) acc[l] = 0.0;
     for (int i0 = 0; i0 < Bs; i0 += 32) {
-      const int vrow = batch_rows_lane(ord + r0, 0, i0, Bs);  // lane u: row of column i0+u
+      // lane u: address of the row of column i0+u (columns past Bs: the clamped row), formed
+      // once per lane and broadcast as two 32-bit halves (no per-row 64-bit SALU multiply)
+      const RowPtr rp(C.phi + koff, idx_l[min(i0 + (tid & 63), Bs - 1)], rstride);   // P0's rows
       double p[32];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) {
-        const int row = __builtin_amdgcn_readlane(vrow, u);  // columns past Bs: clamped row
-        p[u] = (gptr(C.phi) + koff + (long long)row * rstride)[jc];
-      }
+      for (int u = 0; u < 32; ++u) p[u] = GPT_EXP_P2NOLOAD ? 1e-3 * (u + jc) : rp.at(u)[jc];
 #pragma unroll
       for (int u = 0; u < 32; ++u)
 #pragma unroll
