@@ -908,7 +908,7 @@ static int host_sampler(const gpt_sgld_config* cfg, const double* phi, const dou
   int32_t st = 0;
   rc = gpt_sgld_session_fetch(s, 0, w_store, U_store, diag, &st);
   if (rc != GPT_OK) return rc;
-  if (st == 2) {                             // split engine: an in-kernel barrier timed out
+  if (st == GPT_ERR_HIP) {                   // split engine: an in-kernel barrier timed out
     set_error("split engine: the batch-slice barrier timed out (grid not resident)");
     return GPT_ERR_HIP;
   }

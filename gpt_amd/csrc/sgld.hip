@@ -401,7 +401,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1ll << 26)) {             // never expected: a barrier that cannot close
-          __hip_atomic_store(C.status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(C.status, GPT_ERR_HIP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }

@@ -114,7 +114,8 @@ class SGLDSession:
                                                   C.c_void_p(U_out.data_ptr())))
 
     def status(self, chain):
-        """GPT_OK, or GPT_ERR_NAN_GEODESIC when chain hit the geodesic bail-out (4 bytes copied)."""
+        """GPT_OK, GPT_ERR_NAN_GEODESIC when chain hit the geodesic bail-out, or GPT_ERR_HIP when a
+        split-engine barrier timed out (4 bytes copied)."""
         st = C.c_int32(0)
         check(lib().gpt_sgld_session_fetch(self._h, chain, None, None, None, C.byref(st)))
         return st.value

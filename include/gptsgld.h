@@ -158,7 +158,8 @@ int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out);
  * *event_us = the launch's hipEvent time. */
 int64_t gpt_sgld_timeline_slots(void);
 int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, int64_t* out, double* event_us);
-/* Copy chain c's stores / status back (status: GPT_OK or GPT_ERR_NAN_GEODESIC). */
+/* Copy chain c's stores / status back (status: GPT_OK, GPT_ERR_NAN_GEODESIC, or GPT_ERR_HIP when a
+ * split-engine batch-slice barrier timed out; stores are zero-filled for a non-zero status). */
 int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double* w_store, double* U_store,
                            double* diag, int32_t* status);
 void gpt_sgld_session_destroy(gpt_sgld_session* s);
