@@ -190,6 +190,9 @@ CASES = {
     "d1": (32, 1, 30, 3, 3, 7, 0, 2, 1, True, True),
     "n17_odd": (17, 3, 40, 2, 6, 8, 0, 2, 1, True, True),
     "n101_odd": (101, 2, 33, 3, 9, 10, 0, 2, 1, True, True),
+    # more than 8 input dimensions: the grid engine's lane-per-q V-phase tile (the column-lane
+    # form and the chain engine stop at D = 8), split into slices of 7 / 8 rows
+    "d12": (40, 12, 80, 2, 24, 15, 0, 2, 1, True, True),
 }
 
 
