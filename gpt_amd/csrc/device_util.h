@@ -328,15 +328,19 @@ __device__ __forceinline__ void vphase_tile(const double* temp_l, int MP, const 
 // the LDS table entry of q (vphase_cols_tables, 16 ints) is three broadcast reads: the 8 temp row offsets
 // of its factors — the D−1 factors k ≠ kown in k order, ones-row padding, the kown factor last —
 // and I[q, kown].  val[1+l] gets the leave-one-out product, val[0] = that product · temp[kown]
-// (the w block's table has all D factors in k order).  Four entries per pass keep 32 LDS reads
-// in flight.  The per-wave partial sums (NC per column) meet in vred (kNW·NC·64 doubles) and are
+// (the w block's table has all D factors in k order).  VPHASE_QU entries per pass (one measured
+// fastest: the eight reads of one entry are in flight together, more entries only lengthen the
+// pass).  The per-wave partial sums (NC per column) meet in vred (kNW·NC·64 doubles) and are
 // summed in wave order.
+#ifndef VPHASE_QU
+#define VPHASE_QU 1          // core entries per pass of vphase_cols (1: 15.6 k cycles, 2: 16.8 k, 4: 17.5 k)
+#endif
 template <int R, bool WITHA, class Out>
 __device__ __forceinline__ void vphase_cols(const double* temp_l, const int32_t* tab,
                                             const double* w_l, int Q, int Bt, double* vred,
                                             Out out) {
   constexpr int NC = WITHA ? 1 + R : 1;
-  constexpr int QU = 4;
+  constexpr int QU = VPHASE_QU;
   const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   const int Qw = (Q + kNW - 1) / kNW;
   const int qa = wv * Qw, qb = min(Q, qa + Qw);
