@@ -111,7 +111,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       temp_l[o] = i < Bs ? gptr(tsrc)[row * m + i] : 0.0;
     }
     for (int i = tid; i < MP; i += kNT) res_l[i] = 0.0;
-    for (int o = tid; o < Q * D; o += kNT) IT_l[o] = gptr(P.I0)[o];   // I0 is already q + Q*k
+    if (!(vcols && k < D))       // read by the w block's gradw and vphase_tile only
+      for (int o = tid; o < Q * D; o += kNT) IT_l[o] = gptr(P.I0)[o];   // I0 is already q + Q*k
     // RMSprop U phase: A uses the new w written by the w phase (GPT_SGLD.jl:1193-1199)
     const double* wsrc = C.w + (size_t)(((P.rms && k < D) ? t + 1 : t) & 1) * Q;
     for (int q = tid; q < Q; q += kNT) w_l[q] = gptr(wsrc)[q];
