@@ -178,6 +178,12 @@ struct Butterfly {
   __device__ __forceinline__ static void run(double (&v)[NV], int lane) { round<0>(v, lane); }
 };
 
+template <int R, int ICHX = 8>
+struct RCfgX {
+  static constexpr int ICH = (64 / R) < ICHX ? (64 / R) : ICHX;   // batch columns per wave pass
+  static constexpr int NVR = ICH * R;
+  static constexpr int NV = NVR <= 8 ? 8 : (NVR <= 16 ? 16 : (NVR <= 32 ? 32 : 64));
+};
 template <int R>
 struct RCfg {
   static constexpr int ICH = (64 / R) < 8 ? (64 / R) : 8;   // batch columns per wave pass
@@ -215,12 +221,12 @@ struct RowPtr {
   }
 };
 
-template <int R, class Out>
+template <int R, class Out, int ICHX = 8>
 __device__ __forceinline__ void phidotU_tile(const double* __restrict__ phi, long long koff,
                                              long long rstride, const int32_t* ordp, int rowbase,
                                              int Bt, int n, int NP, int NS, const double* U_l,
                                              Out out) {
-  using C = RCfg<R>;
+  using C = RCfgX<R, ICHX>;
   const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   constexpr int SH = 6 - Butterfly<C::NV>::P;
   for (int base = 0; base < Bt; base += kNW * C::ICH) {

@@ -589,8 +589,22 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     __syncthreads();
     STAMP(9);
     double* tdst = C.temp + (size_t)(t1 & 1) * D * R * m + (size_t)k * R * m + r0n;
-    phidotU_tile<R>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS, U_l,
-                    [&](int l, int i, double v) { gptr_w(tdst)[l * m + i] = v; });
+    auto p5out = [&](int l, int i, double v) { gptr_w(tdst)[l * m + i] = v; };
+    // the fewest batch columns per wave pass that cover the (slice of the) next batch in one pass
+    // (fewer row loads, and at <= 32 values a half-size butterfly)
+    if constexpr (RCfgX<R, 4>::ICH != RCfgX<R, 8>::ICH) {
+      if (Bsn <= kNW * RCfgX<R, 4>::ICH) {
+        phidotU_tile<R, decltype(p5out), 4>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS,
+                                            U_l, p5out);
+      } else if (Bsn <= kNW * RCfgX<R, 7>::ICH) {
+        phidotU_tile<R, decltype(p5out), 7>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS,
+                                            U_l, p5out);
+      } else {
+        phidotU_tile<R>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS, U_l, p5out);
+      }
+    } else {
+      phidotU_tile<R>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS, U_l, p5out);
+    }
     __syncthreads();
     STAMP(10);
   }
