@@ -440,6 +440,52 @@ __device__ __forceinline__ void blk_gram(const double* X, const double* Y, int N
   __syncthreads();
 }
 
+// blk_gram's outputs formed row-parallel (R <= 8): thread t takes rows j = t + kNT·x, forms its
+// products for every output, and each wave reduces them with one butterfly; the per-wave totals
+// meet in red (kNW·NVG doubles) and are summed in wave order by the threads that own an output.
+// Same modes and outputs as blk_gram; far shorter dependency chains than its lane-per-output
+// j loops.  Two block barriers.
+template <int R>
+__device__ __forceinline__ void blk_gram_rows(const double* X, const double* Y, int NP, int n,
+                                              int mode, double* out, double* red) {
+  static_assert(R <= 8, "row-parallel Gram: R <= 8");
+  constexpr int NVG = 2 * R * R <= 8 ? 8 : (2 * R * R <= 16 ? 16 : (2 * R * R <= 32 ? 32 : 64));
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
+  const int nout = mode == 0 ? R * R : (mode == 1 ? 2 * R * R : R);
+  double v[NVG];
+#pragma unroll
+  for (int x = 0; x < NVG; ++x) v[x] = 0.0;
+  for (int j = threadIdx.x; j < n; j += kNT) {
+    double xa[R], yb[R];
+#pragma unroll
+    for (int a = 0; a < R; ++a) { xa[a] = X[a * NP + j]; yb[a] = Y[a * NP + j]; }
+    if (mode == 2) {
+#pragma unroll
+      for (int a = 0; a < R; ++a) v[a] = fma(xa[a], xa[a], v[a]);
+    } else {
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = 0; b < R; ++b) {
+          v[a * R + b] = fma(xa[a], yb[b], v[a * R + b]);
+          if (2 * R * R <= NVG && mode == 1) v[R * R + a * R + b] = fma(yb[a], yb[b], v[R * R + a * R + b]);
+        }
+    }
+  }
+  constexpr int SH = 6 - Butterfly<NVG>::P;
+  Butterfly<NVG>::run(v, lane);
+  const int vi = lane >> SH;
+  if ((lane & ((1 << SH) - 1)) == 0 && vi < nout) red[wv * NVG + vi] = v[0];
+  __syncthreads();
+  for (int o = threadIdx.x; o < nout; o += kNT) {
+    double sacc = 0.0;
+#pragma unroll
+    for (int w = 0; w < kNW; ++w) sacc += red[w * NVG + o];
+    out[o] = sacc;
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------- small dense algebra (1 wave)
 // Padé numerator coefficients b_0..b_m of degrees 3, 5, 7, 9 (Higham 2005, Julia Base expm!).
 __constant__ double kPade[4][10] = {

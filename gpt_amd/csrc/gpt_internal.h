@@ -105,7 +105,9 @@ GPT_HD StepLayout step_layout(int n, int D, int r, int Q, int m) {
   L.o_mx = o;   o = al16(o + 8 * (size_t)(r * r));
   L.o_un = o;
   const size_t nrp = 8 * (size_t)r * L.NS;
-  const size_t red = 8 * (size_t)kNW * (2 * r * r > 8 ? 2 * r * r : 8);
+  // Gram scratch: kNW rows of 2r² (blk_gram), padded to the butterfly width of blk_gram_rows
+  const int g2 = 2 * r * r, g2p = g2 <= 8 ? 8 : (g2 <= 16 ? 16 : (g2 <= 32 ? 32 : (g2 <= 64 ? 64 : g2)));
+  const size_t red = 8 * (size_t)kNW * g2p;
   const size_t x0 = 8 * (size_t)7 * 4 * r * r, x1 = 8 * (size_t)7 * r * r;
   L.o_temp = o;
   L.o_W = o;

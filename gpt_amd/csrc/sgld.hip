@@ -30,6 +30,9 @@ namespace gpt {
 #ifndef VPHASE_COLS
 #define VPHASE_COLS 1     // the column-lane V-phase (vphase_cols) where the LDS has its scratch
 #endif
+#ifndef GPT_GRAM_ROWS
+#define GPT_GRAM_ROWS 1     // the projection's Gram row-parallel (blk_gram_rows) at r <= 8
+#endif
 #ifndef GPT_EXP_P2NOLOAD
 #define GPT_EXP_P2NOLOAD 0   // diagnostics only (wrong results): P2 without its row loads
 #endif
@@ -481,10 +484,10 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     double* Mg = gram;              // r×r   Uᵀ·drive
     double* Ag = gram + R * R;      // r×r   Uᵀ·mom
     double* Sg = gram + 2 * R * R;  // r×r   momᵀ·mom
-    double* nrm = gram + 3 * R * R; // r
     int* flag = (int*)(gram + 3 * R * R + R);
     // ---- proj (GPT_SGLD.jl:14-16): mom = V − U(UᵀV + VᵀU)/2
-    blk_gram<R>(U_l, W_l, NS, n, 0, Mg, red);
+    if constexpr (R <= 8 && GPT_GRAM_ROWS) blk_gram_rows<R>(U_l, W_l, NS, n, 0, Mg, red);
+    else blk_gram<R>(U_l, W_l, NS, n, 0, Mg, red);
     for (int j = tid; j < n; j += kNT) {
       double vj[R], uj[R];
 #pragma unroll
@@ -500,7 +503,9 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     __syncthreads();
     STAMP(5);
     // ---- geod (GPT_SGLD.jl:19-37): A = Uᵀmom, S = momᵀmom
-    blk_gram<R>(U_l, W_l, NS, n, 1, Ag, red);      // Ag = Uᵀmom and Sg = momᵀmom in one pass
+    // Ag = Uᵀmom and Sg = momᵀmom in one pass (lane-per-output: the row-parallel form's 64-value
+    // butterfly measured slower here, 5.3 k vs 5.1 k cycles)
+    blk_gram<R>(U_l, W_l, NS, n, 1, Ag, red);
     STAMP(6);
     const double tt = sk;
     const int nn = 2 * R;
@@ -537,35 +542,90 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       if (tid == 0) __hip_atomic_store(C.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
-    // tmpU = ([U mom]·E[:,1:r])·expm(-tA)   (old U re-read from HBM/L2; mom in W_l)
-    for (int j = tid; j < n; j += kNT) {
-      double x[2 * R];
-#pragma unroll
-      for (int l = 0; l < R; ++l) {
-        x[l] = L.keepU ? U_l[l * NS + j] : gptr(Ug)[j + (size_t)n * l];
-        x[R + l] = W_l[l * NS + j];
+    if constexpr (R <= 8) {
+      // tmpU = ([U mom]·E[:,1:r])·expm(-tA)   (old U re-read from HBM/L2; mom in W_l); each thread
+      // keeps the squares of its rows, the column norms are one butterfly per wave and a wave-order
+      // sum (no Gram pass over W_l), and a thread normalises the rows it wrote
+      constexpr int NVN = R <= 8 ? 8 : (R <= 16 ? 16 : 32);
+      double sq2[NVN];
+  #pragma unroll
+      for (int l = 0; l < NVN; ++l) sq2[l] = 0.0;
+      for (int j = tid; j < n; j += kNT) {
+        double x[2 * R];
+  #pragma unroll
+        for (int l = 0; l < R; ++l) {
+          x[l] = L.keepU ? U_l[l * NS + j] : gptr(Ug)[j + (size_t)n * l];
+          x[R + l] = W_l[l * NS + j];
+        }
+        double row1[R];
+  #pragma unroll
+        for (int l = 0; l < R; ++l) {
+          double s = 0.0;
+  #pragma unroll
+          for (int a = 0; a < 2 * R; ++a) s = fma(x[a], Ec[a * R + l], s);
+          row1[l] = s;
+        }
+  #pragma unroll
+        for (int l = 0; l < R; ++l) {
+          double s = 0.0;
+  #pragma unroll
+          for (int c2 = 0; c2 < R; ++c2) s = fma(row1[c2], mx[c2 * R + l], s);
+          W_l[l * NS + j] = s;
+          sq2[l] = fma(s, s, sq2[l]);
+        }
       }
-      double row1[R];
-#pragma unroll
-      for (int l = 0; l < R; ++l) {
-        double s = 0.0;
-#pragma unroll
-        for (int a = 0; a < 2 * R; ++a) s = fma(x[a], Ec[a * R + l], s);
-        row1[l] = s;
+      {
+        constexpr int SHN = 6 - Butterfly<NVN>::P;
+        const int ln = tid & 63;
+        Butterfly<NVN>::run(sq2, ln);
+        const int vi = ln >> SHN;
+        if ((ln & ((1 << SHN) - 1)) == 0 && vi < R) red[wv * NVN + vi] = sq2[0];
       }
-#pragma unroll
+      __syncthreads();
+      double cn[R];
+  #pragma unroll
       for (int l = 0; l < R; ++l) {
-        double s = 0.0;
-#pragma unroll
-        for (int c2 = 0; c2 < R; ++c2) s = fma(row1[c2], mx[c2 * R + l], s);
-        W_l[l * NS + j] = s;
+        double a = 0.0;
+  #pragma unroll
+        for (int w = 0; w < kNW; ++w) a += red[w * NVN + l];
+        cn[l] = sqrt(a);
       }
-    }
-    __syncthreads();
-    blk_gram<R>(W_l, W_l, NS, n, 2, nrm, red);
-    for (int o = tid; o < R * NP; o += kNT) {
-      const int l = o / NP, j = o - l * NP;
-      U_l[l * NS + j] = j < n ? W_l[l * NS + j] / sqrt(nrm[l]) : 0.0;
+      for (int j = tid; j < NP; j += kNT) {
+  #pragma unroll
+        for (int l = 0; l < R; ++l) U_l[l * NS + j] = j < n ? W_l[l * NS + j] / cn[l] : 0.0;
+      }
+    } else {   // r > 8: the Gram pass (the butterfly's partials would spill)
+      // tmpU = ([U mom]·E[:,1:r])·expm(-tA)   (old U re-read from HBM/L2; mom in W_l)
+      for (int j = tid; j < n; j += kNT) {
+        double x[2 * R];
+  #pragma unroll
+        for (int l = 0; l < R; ++l) {
+          x[l] = L.keepU ? U_l[l * NS + j] : gptr(Ug)[j + (size_t)n * l];
+          x[R + l] = W_l[l * NS + j];
+        }
+        double row1[R];
+  #pragma unroll
+        for (int l = 0; l < R; ++l) {
+          double s = 0.0;
+  #pragma unroll
+          for (int a = 0; a < 2 * R; ++a) s = fma(x[a], Ec[a * R + l], s);
+          row1[l] = s;
+        }
+  #pragma unroll
+        for (int l = 0; l < R; ++l) {
+          double s = 0.0;
+  #pragma unroll
+          for (int c2 = 0; c2 < R; ++c2) s = fma(row1[c2], mx[c2 * R + l], s);
+          W_l[l * NS + j] = s;
+        }
+      }
+      __syncthreads();
+      double* nrm = gram + 3 * R * R; // r
+      blk_gram<R>(W_l, W_l, NS, n, 2, nrm, red);
+      for (int o = tid; o < R * NP; o += kNT) {
+        const int l = o / NP, j = o - l * NP;
+        U_l[l * NS + j] = j < n ? W_l[l * NS + j] / sqrt(nrm[l]) : 0.0;
+      }
     }
     __syncthreads();
     STAMP(8);
