@@ -33,6 +33,9 @@ namespace gpt {
 #ifndef GPT_GRAM_ROWS
 #define GPT_GRAM_ROWS 1     // the projection's Gram row-parallel (blk_gram_rows) at r <= 8
 #endif
+#ifndef GPT_EXP_P2NOCOEF
+#define GPT_EXP_P2NOCOEF 0   // diagnostics only (wrong results): P2 without its coefficient reads
+#endif
 #ifndef GPT_EXP_P2NOLOAD
 #define GPT_EXP_P2NOLOAD 0   // diagnostics only (wrong results): P2 without its row loads
 #endif
@@ -372,7 +375,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
 #pragma unroll
       for (int u = 0; u < 32; ++u)
 #pragma unroll
-        for (int l = 0; l < R; ++l) acc[l] = fma(p[u], coef_l[l * MP + i0 + u], acc[l]);
+        for (int l = 0; l < R; ++l)
+          acc[l] = fma(p[u], GPT_EXP_P2NOCOEF ? 1e-3 * (l + u) : coef_l[l * MP + i0 + u], acc[l]);
     }
     if (S > 1) {                  // the slice's partial sums; summed over the slices below
       if (jok) {
