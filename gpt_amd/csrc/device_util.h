@@ -397,6 +397,55 @@ __device__ __forceinline__ void vphase_cols(const double* temp_l, const int32_t*
   }
 }
 
+// vphase_cols for a batch (slice) of at most 32 columns: the two half-waves take alternate core
+// entries (lanes λ and λ + 32 hold the same column), so a wave walks its slice of q in half the
+// passes; the halves' partial sums meet by one permlane swap (even-q sum + odd-q sum).  A's row
+// differs between the halves, so it is selected per lane.
+template <int R, bool WITHA, class Out>
+__device__ __forceinline__ void vphase_cols_half(const double* temp_l, const int32_t* tab,
+                                                 const double* w_l, int Q, int Bt, double* vred,
+                                                 Out out) {
+  constexpr int NC = WITHA ? 1 + R : 1;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6), h = lane >> 5;
+  const int Qw = (Q + kNW - 1) / kNW;
+  const int qa = wv * Qw, qb = min(Q, qa + Qw);
+  const double* tcol = temp_l + min(lane & 31, Bt - 1);
+  double f = 0.0, a[R];
+#pragma unroll
+  for (int l = 0; l < R; ++l) a[l] = 0.0;
+  for (int q0 = qa; q0 < qb; q0 += 2) {
+    const bool ok = q0 + h < qb;
+    const int q = ok ? q0 + h : q0;
+    const int4 e0 = *(const int4*)(tab + 16 * q), e1 = *(const int4*)(tab + 16 * q + 4);
+    const double wq = ok ? w_l[q] : 0.0;
+    const double t0 = tcol[e0.x], t1 = tcol[e0.y], t2 = tcol[e0.z], t3 = tcol[e0.w];
+    const double t4 = tcol[e1.x], t5 = tcol[e1.y], t6 = tcol[e1.z], t7 = tcol[e1.w];
+    const double vk = ((((((t0 * t1) * t2) * t3) * t4) * t5) * t6);
+    f = fma(wq, vk * t7, f);
+    if (WITHA) {
+      const int lk = tab[16 * q + 8];
+      const double cc = wq * vk;
+#pragma unroll
+      for (int l = 0; l < R; ++l) a[l] += (l == lk) ? cc : 0.0;
+    }
+  }
+  f = self_sum<32>(f, lane);
+  vred[wv * NC * 64 + lane] = f;
+  if (WITHA) {
+#pragma unroll
+    for (int l = 0; l < R; ++l) vred[(wv * NC + 1 + l) * 64 + lane] = self_sum<32>(a[l], lane);
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < NC * 64; o += kNT) {
+    const int comp = o >> 6, ln = o & 63;
+    double sacc = 0.0;
+#pragma unroll
+    for (int w = 0; w < kNW; ++w) sacc += vred[(w * NC + comp) * 64 + ln];
+    if (ln < Bt) out(comp, ln, sacc);
+  }
+  __syncthreads();
+}
+
 // Gram products over j < n of LDS rows (stride NP), lanes = outputs, waves = j slices.
 //  mode 0: out[a*R+b] = Σ_j X[a][j]·Y[b][j]                      (R² outputs)
 //  mode 1: out[a*R+b] = Σ X[a]Y[b];  out[R²+a*R+b] = Σ Y[a]Y[b]   (2R² outputs)

@@ -30,6 +30,9 @@ namespace gpt {
 #ifndef VPHASE_COLS
 #define VPHASE_COLS 1     // the column-lane V-phase (vphase_cols) where the LDS has its scratch
 #endif
+#ifndef GPT_VHALF
+#define GPT_VHALF 1         // vphase_cols_half for batches / slices of <= 32 columns
+#endif
 #ifndef GPT_GRAM_ROWS
 #define GPT_GRAM_ROWS 1     // the projection's Gram row-parallel (blk_gram_rows) at r <= 8
 #endif
@@ -161,8 +164,14 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     if (vcols) {
       double* vred = (double*)(smem + L.o_vred);
       const int32_t* tab = (const int32_t*)(smem + L.o_vtab);
-      if (k < D) vphase_cols<R, true>(temp_l, tab, w_l, Q, Bs, vred, vout);
-      else vphase_cols<R, false>(temp_l, tab, w_l, Q, Bs, vred, vout);
+      if (Bs <= 32 && GPT_VHALF) {        // a split slice or a small batch: two q per pass
+        if (k < D) vphase_cols_half<R, true>(temp_l, tab, w_l, Q, Bs, vred, vout);
+        else vphase_cols_half<R, false>(temp_l, tab, w_l, Q, Bs, vred, vout);
+      } else if (k < D) {
+        vphase_cols<R, true>(temp_l, tab, w_l, Q, Bs, vred, vout);
+      } else {
+        vphase_cols<R, false>(temp_l, tab, w_l, Q, Bs, vred, vout);
+      }
     } else if (Bs <= kNW * VCfg<R>::ICV_SMALL)
       vphase_tile<R, VCfg<R>::ICV_SMALL>(temp_l, MP, IT_l, w_l, Q, D, k >= D ? 0 : k, Bs, vout);
     else
