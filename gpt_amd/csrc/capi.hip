@@ -219,13 +219,18 @@ struct gpt_sgld_session {
 // Without a forced choice, few chains go to the grid engine (D+1 workgroups per chain: the shorter
 // step) as long as every chain's workgroups fit the GPU at once; more chains go to the chain engine
 // (one workgroup per chain, one batch read per step: the higher throughput).
-// Batch slices per dimension of the split engine: the largest S <= 8 whose D·S + 1 workgroups
-// per chain all fit the GPU at once (the in-kernel barrier needs the whole grid resident) with
-// at least 6 rows per slice; GPTSGLD_SPLIT=S overrides (S >= 2, still subject to residency).
+// Batch slices per dimension of the split engine: the smallest S >= 2 whose slices have at most
+// 32 rows (the half-wave V-phase, vphase_cols_half; more slices only add barrier partners:
+// scripts/single_chain.py measured S = 2 fastest at m = 50), at most 8, with all D·S + 1
+// workgroups per chain resident at once (the in-kernel barrier needs the whole grid) and at least
+// 6 rows per slice; GPTSGLD_SPLIT=S overrides (S >= 2, still subject to residency).
 static int split_factor(int nchains, int D, int m, int cus) {
   int S = 1;
   for (int s2 = 2; s2 <= 8; ++s2)
-    if ((long long)nchains * (D * s2 + 1) <= cus && m / s2 >= 6) S = s2;
+    if ((long long)nchains * (D * s2 + 1) <= cus && m / s2 >= 6) {
+      S = s2;
+      if ((m + s2 - 1) / s2 <= 32) break;
+    }
   if (const char* ev = std::getenv("GPTSGLD_SPLIT")) {
     const int v = std::atoi(ev);
     if (v >= 1 && (long long)nchains * (D * v + 1) <= cus) S = v;
