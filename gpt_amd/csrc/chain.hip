@@ -41,6 +41,15 @@ namespace gpt {
 #ifndef CHAIN_TOUCH               // next-batch rows pulled into L2 / Infinity Cache during the
 #define CHAIN_TOUCH 0             // Stiefel phase (rows per dimension; 0 = off)
 #endif
+#ifndef CHAIN_GRAM_MODE           // proj / geod Grams: M and G in one pass (0), M then momᵀmom (2)
+#define CHAIN_GRAM_MODE 2
+#endif
+#ifndef CHAIN_SCTAB               // U-noise angles from an LDS sin/cos table (1) or by polynomial (0)
+#define CHAIN_SCTAB 1
+#endif
+#ifndef CHAIN_OBF                 // (b) butterfly over exactly G·R values (1) or padded to 2^k (0)
+#define CHAIN_OBF 1
+#endif
 #ifndef CHAIN_BFLY
 #define CHAIN_BFLY 1              // (b) reduction: register butterfly (1) or LDS scratch + 8-lane DPP (0)
 #endif
@@ -100,7 +109,11 @@ struct ChainLds {
   // stays under 80 KB, two chains per CU)
   static constexpr int L_dbl = G * kChainQS + WV * G * R * kChainRunS;
   static constexpr int x_dbl = chain_scratch_dbl(R);
-  static constexpr int bytes = al16c(o_un + 8 * (L_dbl > x_dbl * WV ? L_dbl : x_dbl * WV));
+  // after the union: the U noise's (sin, cos)(2πi/256) table (WV = 8 builds; the WV = 4 carve
+  // stays under 80 KB for two chains per CU and draws its angles by polynomial)
+  static constexpr int o_tab = al16c(o_un + 8 * (L_dbl > x_dbl * WV ? L_dbl : x_dbl * WV));
+  static constexpr bool tab = CHAIN_SCTAB && WV == kChainDMax;
+  static constexpr int bytes = al16c(o_tab + (tab ? 8 * 512 : 0));
 };
 
 // Timeline of every workgroup in P.stamps (gpt_sgld_session_timeline; kTimeline slots per block).
@@ -313,6 +326,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     }
     for (int o = tid; o < kChainQPL * G; o += NTH) fp_l[o] = 0.0;
   }
+  if constexpr (L::tab) sincos_tab_fill((double*)(smem + L::o_tab), tid, NTH);
   for (int q = tid; q < Q; q += NTH) w_l[q] = gptr(Cp->w)[(size_t)(t0 & 1) * Q + q];
   if (tid == 0) flag[0] = 0;
   {
@@ -419,20 +433,32 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     {
       // the G·R partial dots of this lane, reduced over the wave by one register butterfly
       // (permlane swaps + DPP, no LDS round trip): lane λ ends with the total of value λ >> SH
-      constexpr int NVB = G * R <= 8 ? 8 : (G * R <= 16 ? 16 : (G * R <= 32 ? 32 : 64));
-      constexpr int SH = 6 - Butterfly<NVB>::P;
-      double v[NVB];
+      double v[G * R];
 #pragma unroll
-      for (int x = 0; x < NVB; ++x) v[x] = 0.0;
+      for (int x = 0; x < G * R; ++x) v[x] = 0.0;
 #pragma unroll
       for (int gg = 0; gg < G; ++gg)
 #pragma unroll
         for (int jj = 0; jj < J; ++jj)
 #pragma unroll
           for (int l = 0; l < R; ++l) v[gg * R + l] = fma(p[gg][jj], u[jj][l], v[gg * R + l]);
-      Butterfly<NVB>::run(v, ln);
+#if CHAIN_OBF
+      obf_run<G * R, G * R>(v, ln);
+      int vi;
+      bool wr;
+      obf_index<G * R>(ln, vi, wr);
+      if (wr) {
+#else
+      constexpr int NVB = G * R <= 8 ? 8 : (G * R <= 16 ? 16 : (G * R <= 32 ? 32 : 64));
+      constexpr int SH = 6 - Butterfly<NVB>::P;
+      double vb[NVB];
+#pragma unroll
+      for (int x = 0; x < NVB; ++x) vb[x] = x < G * R ? v[x] : 0.0;
+      Butterfly<NVB>::run(vb, ln);
+      v[0] = vb[0];
       const int vi = ln >> SH;
       if ((ln & ((1 << SH) - 1)) == 0 && vi < G * R) {
+#endif
         const int gg = vi / R, l = vi - gg * R;
         tsl[(k * R + l) * G + gg] = v[0];
         tsl[DRG + G + (k * R + l) * G + gg] = rcp_nr(v[0]);
@@ -656,8 +682,12 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         if (CHAIN_EXP_NONOISE) {
           z[0] = z[1] = z[2] = z[3] = 0.0;
         } else {
-          normal_quad<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
-                          (uint32_t)k, z);
+          if constexpr (L::tab)
+            normal_quad_tab<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
+                                (uint32_t)k, (const double*)(smem + L::o_tab), z);
+          else
+            normal_quad<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
+                            (uint32_t)k, z);
         }
 #pragma unroll
         for (int i = 0; i < NZ; ++i)
@@ -694,18 +724,28 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     double* Sg = Ag + R * R;
     double* nr = Sg + R * R;
     wave_sync();                             // noise slots (aliasing X0) are consumed
-    // proj (GPT_SGLD.jl:14-16): mom = W − U(UᵀW + WᵀU)/2
+    // proj (GPT_SGLD.jl:14-16): M = UᵀW, mom = W − U·Ms with Ms = (M + Mᵀ)/2; geod (:19-37)
+    // needs A = Uᵀmom and S = momᵀmom.  With UᵀU = I, A = (M − Mᵀ)/2 and
+    // S = G − MᵀMs − Ms·M + Ms·Ms for the drive's Gram G = WᵀW (the oracle's reference form
+    // agrees to ≤ 1.2e-14 relative over whole trajectories, tests/test_oracle.py), so Uᵀmom
+    // needs no pass over the rows.  CHAIN_GRAM_MODE 0: M and G from one pass (row a reduces
+    // M[a,:] and G[a,a:] in one butterfly); 2: M, then S = momᵀmom from a second pass after mom.
 #pragma unroll
     for (int a = 0; a < R; ++a) {
-      double v[R];
+      double v[2 * R];
 #pragma unroll
       for (int bb = 0; bb < R; ++bb) {
-        double s = 0.0;
+        double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-        for (int jj = 0; jj < J; ++jj) s = fma(u[jj][a], acc[jj][bb], s);
-        v[bb] = s;
+        for (int jj = 0; jj < J; ++jj) {
+          s0 = fma(u[jj][a], acc[jj][bb], s0);
+          if (CHAIN_GRAM_MODE == 0 && bb >= a) s1 = fma(acc[jj][a], acc[jj][bb], s1);
+        }
+        v[bb] = s0;
+        v[R + bb] = s1;
       }
-      wave_sum_to_lds<R>(v, Mg + a * R);
+      if constexpr (CHAIN_GRAM_MODE == 0) wave_sum_to_lds<R>(v, Mg + a * R, Sg + a * R);
+      else wave_sum_to_lds<R>(*(double(*)[R])v, Mg + a * R);
     }
     wave_sync();
     SSTAMP(5);
@@ -722,26 +762,47 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         acc[jj][bb] = acc[jj][bb] - s / 2;
       }
     }
-      // geod (GPT_SGLD.jl:19-37): A = Uᵀmom, S = momᵀmom, E = expm(t[A −S; I A]), expm(−tA)
-#pragma unroll
-      for (int a = 0; a < R; ++a) {
-        double v[2 * R];
-#pragma unroll
-        for (int bb = 0; bb < R; ++bb) {
-          double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-          for (int jj = 0; jj < J; ++jj) {
-            s0 = fma(u[jj][a], acc[jj][bb], s0);
-            s1 = fma(acc[jj][a], acc[jj][bb], s1);
-          }
-          v[bb] = s0;
-          v[R + bb] = s1;
-        }
-        wave_sum_to_lds<R>(v, Ag + a * R, Sg + a * R);
-      }
-      wave_sync();
       CSTAMP(5);
       SSTAMP(6);
+      if constexpr (CHAIN_GRAM_MODE == 2) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          double v[R];
+#pragma unroll
+          for (int bb = 0; bb < R; ++bb) {
+            double s1 = 0.0;
+            if (bb >= a)
+#pragma unroll
+              for (int jj = 0; jj < J; ++jj) s1 = fma(acc[jj][a], acc[jj][bb], s1);
+            v[bb] = s1;
+          }
+          wave_sum_to_lds<R>(v, Sg + a * R);    // S[a][b] valid for b >= a
+        }
+        wave_sync();
+        for (int o = lane; o < R * R; o += 64) {
+          const int i = o / R, b = o - i * R;
+          Ag[o] = (Mg[o] - Mg[b * R + i]) / 2;
+          if (i > b) Sg[o] = Sg[b * R + i];
+        }
+      } else {
+        // lanes < r² form A[i][b] and S[i][b] (a short loop: U and the drive stay in registers)
+        if (lane < R * R) {
+          const int i = lane / R, b = lane - i * R;
+          double s = Sg[min(i, b) * R + max(i, b)];
+#pragma unroll 1
+          for (int c = 0; c < R; ++c) {
+            const double mci = Mg[c * R + i], mic = Mg[i * R + c];
+            const double mcb = Mg[c * R + b], mbc = Mg[b * R + c];
+            const double msic = (mic + mci) / 2, mscb = (mcb + mbc) / 2;
+            s = fma(-mci, mscb, s);
+            s = fma(-msic, mcb, s);
+            s = fma(msic, mscb, s);
+          }
+          Ag[lane] = (Mg[lane] - Mg[b * R + i]) / 2;
+          Sg[lane] = s;                       // after this wave's G reads (in-order LDS)
+        }
+      }
+      wave_sync();
       const double tt = sq;
       for (int o = lane; o < NN * NN; o += 64) {
         const int i = o / NN, j = o - i * NN;

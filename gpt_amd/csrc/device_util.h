@@ -178,6 +178,37 @@ struct Butterfly {
   __device__ __forceinline__ static void run(double (&v)[NV], int lane) { round<0>(v, lane); }
 };
 
+// Butterfly for any count NV of values (no padding to a power of two): at each of the 6 lane
+// stages the NV values pair up (NV/2 exchanges; an odd last value is summed with its partner's
+// copy and kept by both), leaving ⌈NV/2⌉.  For NV = 10 that is 47 VALU instructions against 63
+// for Butterfly<16>.  obf_index gives the value a lane holds in v[0] afterwards and whether the
+// lane is that value's one writer.
+template <int N0, int NV, int S = 0>
+__device__ __forceinline__ void obf_run(double (&v)[N0], int lane) {
+  if constexpr (S < 6) {
+    constexpr int off = 32 >> S, H = NV / 2;
+#pragma unroll
+    for (int u = 0; u < H; ++u) v[u] = pair_sum<off>(v[u], v[u + H], lane);
+    if constexpr (NV & 1) v[H] = self_sum<off>(v[NV - 1], lane);
+    obf_run<N0, H + (NV & 1), S + 1>(v, lane);
+  }
+}
+template <int NV, int S = 0>
+__device__ __forceinline__ void obf_index(int lane, int& idx, bool& wr) {
+  if constexpr (S < 6) {
+    constexpr int H = NV / 2;
+    int j;
+    bool w;
+    obf_index<H + (NV & 1), S + 1>(lane, j, w);
+    const bool bit = ((lane >> (5 - S)) & 1) != 0;
+    if (j < H) { idx = bit ? j + H : j; wr = w; }
+    else { idx = NV - 1; wr = w && !bit; }
+  } else {
+    idx = 0;
+    wr = true;
+  }
+}
+
 template <int R, int ICHX = 8>
 struct RCfgX {
   static constexpr int ICH = (64 / R) < ICHX ? (64 / R) : ICHX;   // batch columns per wave pass

@@ -23,6 +23,7 @@
 namespace gpt {
 
 // [0..6] Lg1..Lg7  [7] ln2_hi  [8] ln2_lo  [9..14] S1..S6  [15..20] C1..C6  [21] π/2 hi  [22] π/2 lo
+// [23] 2π·2⁻³²  [24..26] Taylor sin φ³, φ⁵, φ⁷  [27..30] Taylor cos φ², φ⁴, φ⁶, φ⁸ (fm_sincos_tab)
 #define GPT_FM_COEF                                                                              \
   {6.666666666666735130e-01, 3.999999999940941908e-01, 2.857142874366239149e-01,                 \
    2.222219843214978396e-01, 1.818357216161805012e-01, 1.531383769920937332e-01,                 \
@@ -31,7 +32,10 @@ namespace gpt {
    2.75573137070700676789e-06, -2.50507602534068634195e-08, 1.58969099521155010221e-10,          \
    4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05,          \
    -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11,         \
-   1.57079632679489655800e+00, 6.12323399573676603587e-17}
+   1.57079632679489655800e+00, 6.12323399573676603587e-17,                                     \
+   1.4629180792671596e-09, -1.66666666666666666667e-01, 8.33333333333333333333e-03,          \
+   -1.98412698412698412698e-04, -5.0e-01, 4.16666666666666666667e-02,                           \
+   -1.38888888888888888889e-03, 2.48015873015873015873e-05}
 
 // 1/x: on the device the hardware reciprocal plus two Newton steps (within 1 ulp)
 GPT_HD double fm_rcp(double x) {
@@ -95,6 +99,28 @@ GPT_HD void fm_sincos_2pi_c(double u, double& sn, double& cs, CP c) {
   memcpy(&cs, &bc, 8);
 }
 
+// sin(2πu), cos(2πu) for u = (x + ½)·2⁻³² (the Box–Muller angle of a 32-bit Philox word) from
+// a table of (sin, cos)(2πi/256), i < 256 (tab: 512 doubles, e.g. in LDS; fm_sincos_tab_fill):
+// u = i/256 + δ with i = x >> 24 and δ = ((x mod 2²⁴) + ½)·2⁻³² exact, |2πδ| < 2π/256, where
+// Taylor polynomials of degrees 7 / 8 are exact to < 1e-20; then the angle-sum formulas.  About
+// half the instructions of fm_sincos_2pi_c, within 2 ulp of it.
+template <class CP, class TP>
+GPT_HD void fm_sincos_tab(uint32_t x, const TP* tab, double& sn, double& cs, CP c) {
+  const unsigned i = x >> 24;
+  const double ph = ((double)(x & 0xFFFFFFu) + 0.5) * c[23];
+  const double z = ph * ph;
+  double ts = fma(z, c[26], c[25]);
+  ts = fma(z, ts, c[24]);
+  const double sp = fma(ph * z, ts, ph);
+  double tc = fma(z, c[30], c[29]);
+  tc = fma(z, tc, c[28]);
+  tc = fma(z, tc, c[27]);
+  const double cp = fma(z, tc, 1.0);
+  const double st = tab[2 * i], ct = tab[2 * i + 1];
+  sn = fma(st, cp, ct * sp);
+  cs = fma(ct, cp, -(st * sp));
+}
+
 // √x for finite normal x > 0 (the Box–Muller radius: x = −2 ln u in [2e-10, 46]): on the device
 // the hardware rsq refined by two Newton steps (the refinement of the library expansion without
 // its denormal scaling and class checks).
@@ -115,7 +141,7 @@ GPT_HD double fm_sqrt_pos(double x) {
 }
 
 struct FmHostCoef {
-  double v[23];
+  double v[31];
   GPT_HD double operator[](int i) const { return v[i]; }
 };
 GPT_HD double fm_log(double x) {

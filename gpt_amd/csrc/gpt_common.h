@@ -32,7 +32,13 @@ GPT_HD U4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // three-input xor in one v_bitop3_b32 (gfx950; truth table 0x96)
+    const uint32_t n0 = __builtin_amdgcn_bitop3_b32(hi1, c1, k0, 0x96);
+    const uint32_t n2 = __builtin_amdgcn_bitop3_b32(hi0, c3, k1, 0x96);
+#else
     const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+#endif
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
   }
   return U4{c0, c1, c2, c3};
@@ -42,7 +48,7 @@ GPT_HD double u53(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6) + 0.5) * (1.0 / 9007199254740992.0);
 }
 
-__constant__ double kFmCoef[23] = GPT_FM_COEF;
+__constant__ double kFmCoef[31] = GPT_FM_COEF;
 
 // The Box–Muller coefficient table behind a pointer the compiler cannot see through: the
 // coefficients are scalar-loaded where used rather than hoisted into registers.
@@ -109,6 +115,40 @@ __device__ __forceinline__ void normal_quad(uint64_t seed, uint32_t c0, uint32_t
     fm_sincos_2pi_c(u32u(x.w), sn, cs, c);
     z[2] = rad * cs;
     z[3] = rad * sn;
+  }
+}
+
+// normal_quad with the angles from fm_sincos_tab (table in LDS, filled by sincos_tab_fill): the
+// same streams to within 2 ulp
+template <int NZ>
+__device__ __forceinline__ void normal_quad_tab(uint64_t seed, uint32_t c0, uint32_t c1,
+                                                uint32_t c2, uint32_t c3, const double* tab,
+                                                double* z) {
+  const U4 x = philox4x32(c0, c1, c2, c3, seed);
+  const auto c = fm_coef();
+  {
+    const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.x), c));
+    double sn, cs;
+    fm_sincos_tab(x.y, tab, sn, cs, c);
+    z[0] = rad * cs;
+    z[1] = rad * sn;
+  }
+  if constexpr (NZ == 4) {
+    const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.z), c));
+    double sn, cs;
+    fm_sincos_tab(x.w, tab, sn, cs, c);
+    z[2] = rad * cs;
+    z[3] = rad * sn;
+  }
+}
+// (sin, cos)(2πi/256) for i < 256 into tab[2i], tab[2i + 1]
+__device__ __forceinline__ void sincos_tab_fill(double* tab, int tid, int nth) {
+  const auto c = fm_coef();
+  for (int i = tid; i < 256; i += nth) {
+    double sn, cs;
+    fm_sincos_2pi_c((double)i * (1.0 / 256.0), sn, cs, c);
+    tab[2 * i] = sn;
+    tab[2 * i + 1] = cs;
   }
 }
 

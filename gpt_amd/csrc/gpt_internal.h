@@ -100,7 +100,7 @@ GPT_HD StepLayout step_layout(int n, int D, int r, int Q, int m) {
   L.o_y = o;    o = al16(o + 8 * (size_t)m);
   L.o_res = o;  o = al16(o + 8 * (size_t)L.MP);
   L.o_coef = o; o = al16(o + 8 * (size_t)r * L.MP);
-  L.o_gram = o; o = al16(o + 8 * (size_t)(3 * r * r + r + 2));
+  L.o_gram = o; o = al16(o + 8 * (size_t)(4 * r * r + r + 2));
   L.o_Ec = o;   o = al16(o + 8 * (size_t)(2 * r * r));
   L.o_mx = o;   o = al16(o + 8 * (size_t)(r * r));
   L.o_un = o;

@@ -33,9 +33,6 @@ namespace gpt {
 #ifndef GPT_VHALF
 #define GPT_VHALF 1         // vphase_cols_half for batches / slices of <= 32 columns
 #endif
-#ifndef GPT_GRAM_ROWS
-#define GPT_GRAM_ROWS 1     // the projection's Gram row-parallel (blk_gram_rows) at r <= 8
-#endif
 #ifndef GPT_EXP_P2NOCOEF
 #define GPT_EXP_P2NOCOEF 0   // diagnostics only (wrong results): P2 without its coefficient reads
 #endif
@@ -494,13 +491,36 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     __syncthreads();
   }
   if (pass == 0 ? (P.stiefel || P.ncls) : P.stiefel) {
-    double* Mg = gram;              // r×r   Uᵀ·drive
-    double* Ag = gram + R * R;      // r×r   Uᵀ·mom
-    double* Sg = gram + 2 * R * R;  // r×r   momᵀ·mom
-    int* flag = (int*)(gram + 3 * R * R + R);
-    // ---- proj (GPT_SGLD.jl:14-16): mom = V − U(UᵀV + VᵀU)/2
-    if constexpr (R <= 8 && GPT_GRAM_ROWS) blk_gram_rows<R>(U_l, W_l, NS, n, 0, Mg, red);
-    else blk_gram<R>(U_l, W_l, NS, n, 0, Mg, red);
+    double* Mg = gram;              // r×r   M = Uᵀ·drive
+    double* Gg = gram + R * R;      // r×r   G = driveᵀ·drive
+    double* Ag = gram + 2 * R * R;  // r×r   A = Uᵀ·mom
+    double* Sg = gram + 3 * R * R;  // r×r   S = momᵀ·mom
+    int* flag = (int*)(gram + 4 * R * R + R);
+    // ---- proj (GPT_SGLD.jl:14-16): mom = V − U(UᵀV + VᵀU)/2, and the geod Grams (:19-37).  On the
+    // Stiefel manifold (UᵀU = I: every move of a stiefel run is a geodesic from a Stiefel init) they
+    // come from the same Gram pass: A = Uᵀmom = (M − Mᵀ)/2 and
+    // S = momᵀmom = G − MᵀMs − Ms·M + Ms·Ms (M = UᵀV, G = VᵀV, Ms = (M + Mᵀ)/2), so no second pass
+    // over mom (the oracle's reference form agrees to ≤ 1.2e-14 relative over whole trajectories,
+    // tests/test_oracle.py).  GPTclassification's pass 0 with stiefel = false moves a U that the
+    // Euclidean pass 1 took off the manifold: there A and S come from mom as the reference does.
+    const bool onm = P.stiefel != 0;
+    blk_gram<R>(U_l, W_l, NS, n, onm ? 1 : 0, Mg, red);
+    if (onm) {
+      for (int o = tid; o < R * R; o += kNT) {
+        const int i = o / R, b = o - i * R;
+        double s = Gg[min(i, b) * R + max(i, b)];
+        for (int c = 0; c < R; ++c) {
+          const double mci = Mg[c * R + i], mic = Mg[i * R + c];
+          const double mcb = Mg[c * R + b], mbc = Mg[b * R + c];
+          const double msic = (mic + mci) / 2, mscb = (mcb + mbc) / 2;
+          s = fma(-mci, mscb, s);
+          s = fma(-msic, mcb, s);
+          s = fma(msic, mscb, s);
+        }
+        Sg[o] = s;
+        Ag[o] = (Mg[o] - Mg[b * R + i]) / 2;
+      }
+    }
     for (int j = tid; j < n; j += kNT) {
       double vj[R], uj[R];
 #pragma unroll
@@ -515,10 +535,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     }
     __syncthreads();
     STAMP(5);
-    // ---- geod (GPT_SGLD.jl:19-37): A = Uᵀmom, S = momᵀmom
-    // Ag = Uᵀmom and Sg = momᵀmom in one pass (lane-per-output: the row-parallel form's 64-value
-    // butterfly measured slower here, 5.3 k vs 5.1 k cycles)
-    blk_gram<R>(U_l, W_l, NS, n, 1, Ag, red);
+    if (!onm) blk_gram<R>(U_l, W_l, NS, n, 1, Ag, red);   // Ag = Uᵀmom, Sg = momᵀmom
     STAMP(6);
     const double tt = sk;
     const int nn = 2 * R;
@@ -633,7 +650,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
         }
       }
       __syncthreads();
-      double* nrm = gram + 3 * R * R; // r
+      double* nrm = gram + 4 * R * R; // r
       blk_gram<R>(W_l, W_l, NS, n, 2, nrm, red);
       for (int o = tid; o < R * NP; o += kNT) {
         const int l = o / NP, j = o - l * NP;
