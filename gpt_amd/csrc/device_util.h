@@ -576,10 +576,16 @@ __constant__ double kPade[4][10] = {
      3960.0, 90.0, 1.0}};
 
 // NN is compile-time so every inner product is unrolled with all its LDS reads in flight.
+// wave_mm takes the register-blocked form from this size up (NN = 10, the r = 5 geodesic: 25
+// lanes with 2 × 2 blocks, one pass instead of two passes of 64 + 36 lane-outputs)
+#ifndef GPT_WAVE_MM_BLOCKED
+#define GPT_WAVE_MM_BLOCKED 10
+#endif
+constexpr int kWaveMmBlocked = GPT_WAVE_MM_BLOCKED;
 template <int NN>
 __device__ __forceinline__ void wave_mm(const double* A, const double* B, double* C) {
   const int lane = threadIdx.x & 63;
-  if constexpr (NN >= 16) {
+  if constexpr (NN >= kWaveMmBlocked) {
     // register-blocked: lane (bi, bj) of an NB × NB grid owns a BS × BS block of C, so each LDS
     // value read feeds BS FMAs (NN = 40: 5 × 5 blocks, 0.4 reads per FMA instead of 2).  Every
     // output is still Σ_t A[i,t]·B[t,j] accumulated in t order — the same doubles as below.
