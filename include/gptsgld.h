@@ -82,7 +82,9 @@ int gpt_sgld_init(const gpt_sgld_config* cfg, double* w_out, double* U_out);
 /* ---- sampler ------------------------------------------------------------------------- */
 /* GPTregression(phi,y,signal_var,I,r,Q,m,epsw,epsU,burnin,maxepoch,param_seed;langevin,stiefel)
  * GPT_SGLD.jl:345-448 (also GPT_SGLDERM, GPT_SGLD_p.jl:146-243, via sigma_w/signal_var).
- * w_init/U_init: NULL = draw from the seed (the reference's srand(param_seed) path).
+ * w_init/U_init: NULL = draw from the seed (the reference's srand(param_seed) path).  With
+ * stiefel, U_init must have orthonormal columns per dimension (as the reference's init does): the
+ * geodesic takes Uᵀmom as (M − Mᵀ)/2 from the projection's M = UᵀW, which holds on the manifold.
  * w_store (Q,T), U_store (n,r,D,T) with T = maxepoch*numbatches/store_every.
  * diag (nullable): per step [‖gradw‖, ‖gradU_1‖ … ‖gradU_D‖] ((1+D) x steps). */
 int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi, const double* y,
