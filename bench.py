@@ -534,24 +534,6 @@ def main():
         single = {"steps_per_s": sps, "engine": s1.info()["engine"], "kernel_us": s1_us,
                   "roofline_frac": (b1 / (s1_us * 1e-6) / 1e9 / HBM_PEAK_GBS) if s1_us else None}
         s1.close()
-        if args.engine == "auto":
-            # the opt-in split engine (S batch slices per dimension, in-kernel slice barrier) on
-            # the same chain, reported beside the default
-            from gpt_amd._lib import GPTError
-            try:
-                s2 = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0,
-                                 epochs, [7], store_every=nb, store=False, engine="split")
-                s2.run(args.warmup)
-                s2.prepare(args.steps)
-                s2.sync()
-                t2 = time.perf_counter(); s2.run(args.steps); s2.sync()
-                sps2 = args.steps / (time.perf_counter() - t2)
-                s2_us = s2.time_steps(min(args.kernel_steps, s2.total_steps - s2.steps_done))
-                single["split_engine"] = {"steps_per_s": sps2, "kernel_us": s2_us,
-                                          "workgroups": s2.info()["workgroups"]}
-                s2.close()
-            except GPTError as exc:
-                single["split_engine"] = {"unavailable": str(exc)}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:          # host cores of rank 0's box, any N

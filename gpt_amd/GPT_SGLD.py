@@ -186,8 +186,8 @@ def _engine_env(engine):
     if engine is None:
         yield
         return
-    if engine not in ("grid", "chain", "split", "auto"):
-        raise ValueError("engine must be 'grid', 'chain', 'split' or 'auto'")
+    if engine not in ("grid", "chain", "wave", "auto"):
+        raise ValueError("engine must be 'grid', 'chain', 'wave' or 'auto'")
     old = os.environ.get("GPTSGLD_ENGINE")
     os.environ["GPTSGLD_ENGINE"] = engine
     try:
@@ -204,7 +204,7 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
                   w_init=None, U_init=None, diag=False, engine=None):
     """Tensor-GP regression sampler (GPT_SGLD.jl:345-448).  Returns (w_store, U_store)
     [, diag]; ``diag`` = per-step [‖gradw‖, ‖gradU_1‖, …] ((1+D) × steps).
-    ``engine`` ("grid" | "chain" | "split" | None = library default) selects the step kernel."""
+    ``engine`` ("grid" | "chain" | "wave" | None = library default) selects the step kernel."""
     phi = _f64(phi)
     n, D, N = phi.shape
     y = _f64(np.asarray(y, dtype=np.float64).ravel())

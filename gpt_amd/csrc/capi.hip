@@ -176,7 +176,9 @@ static bool valid_cfg(const gpt_sgld_config* c) {
   const StepLayout L = step_layout((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m);
   const bool chain_ok = chain_supported((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m,
                                         c->langevin != 0, c->stiefel != 0);
-  if (L.bytes > 160 * 1024 && !chain_ok) {
+  const bool wave_ok = wave_supported((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m,
+                                       c->langevin != 0, c->stiefel != 0);
+  if (L.bytes > 160 * 1024 && !chain_ok && !wave_ok) {
     set_error("working set exceeds 160 KiB LDS (n*r, Q*D or m too large)"); return false;
   }
   return true;
@@ -208,36 +210,20 @@ struct gpt_sgld_session {
   int graph_steps = 0;                // canonical chunk: one epoch (<= 512 steps)
   DevMem ord_ws;                      // epoch-order workspace when a shuffle exceeds LDS
   bool store = false, diag = false;
-  int engine = 0;                     // kEngineGrid / kEngineChain / kEngineSplit
+  int engine = 0;                     // kEngineGrid / kEngineChain / kEngineWave
   DevMem runq;
-  DevMem vtab;                        // grid / split engine: vphase_cols tables
+  DevMem wvtab;                       // wave engine: run members and starts (wave_tables)
+  DevMem vtab;                        // grid engine: vphase_cols tables
 };
 
-// Engine choice: store_flags bit 2 (or bit 4, w-only steps) forces the grid engine (sgld.hip), bit 3
-// the chain engine (chain.hip), bit 6 the split engine (sgld.hip, P.split); otherwise
-// GPTSGLD_ENGINE=grid|chain|split, otherwise chain whenever it supports the shape.
-// Without a forced choice, few chains go to the grid engine (D+1 workgroups per chain: the shorter
-// step) as long as every chain's workgroups fit the GPU at once; more chains go to the chain engine
-// (one workgroup per chain, one batch read per step: the higher throughput).
-// Batch slices per dimension of the split engine: the smallest S >= 2 whose slices have at most
-// 32 rows (the half-wave V-phase, vphase_cols_half; more slices only add barrier partners:
-// scripts/single_chain.py measured S = 2 fastest at m = 50), at most 8, with all D·S + 1
-// workgroups per chain resident at once (the in-kernel barrier needs the whole grid) and at least
-// 6 rows per slice; GPTSGLD_SPLIT=S overrides (S >= 2, still subject to residency).
-static int split_factor(int nchains, int D, int m, int cus) {
-  int S = 1;
-  for (int s2 = 2; s2 <= 8; ++s2)
-    if ((long long)nchains * (D * s2 + 1) <= cus && m / s2 >= 6) {
-      S = s2;
-      if ((m + s2 - 1) / s2 <= 32) break;
-    }
-  if (const char* ev = std::getenv("GPTSGLD_SPLIT")) {
-    const int v = std::atoi(ev);
-    if (v >= 1 && (long long)nchains * (D * v + 1) <= cus) S = v;
-  }
-  return S;
-}
-
+// Engine choice: store_flags bit 2 (or bit 4 / 5, w-only steps / classification) forces the grid
+// engine (sgld.hip), bit 3 the chain engine (chain.hip), bit 7 the wave engine (wave.hip);
+// otherwise GPTSGLD_ENGINE=grid|chain|wave; otherwise the chain engine whenever it supports the
+// shape, else the wave engine (ranks past the chain engine), else the grid engine.  Few chains
+// of a chain-engine shape go to the grid engine (D+1 workgroups per chain: the shorter step) as
+// long as every chain's workgroups fit the GPU at once.  (Engine 2, the round-3 split engine —
+// the grid engine with the batch in slices and an in-kernel barrier — measured slower at every
+// slice count and was removed in round 4; bit 6 / "split" are rejected.)
 static int device_cus() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -257,21 +243,25 @@ static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t 
                                         c->langevin != 0, c->stiefel != 0, max_run);
   const bool grid_ok =
       step_layout((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m).bytes <= 160 * 1024;
+  const bool wave_ok = wave_supported((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m,
+                                      c->langevin != 0, c->stiefel != 0);
   int want = -1;
   if (flags & (4 | 16 | 32)) want = kEngineGrid;
   else if (flags & 8) want = kEngineChain;
-  else if (flags & 64) want = kEngineSplit;
+  else if (flags & 128) want = kEngineWave;
+  if (flags & 64) { set_error("the split engine (store_flags bit 6) was removed"); return GPT_ERR_BAD_DIMS; }
   else if (const char* ev = std::getenv("GPTSGLD_ENGINE")) {
     if (!std::strcmp(ev, "grid")) want = kEngineGrid;
     else if (!std::strcmp(ev, "chain")) want = kEngineChain;
-    else if (!std::strcmp(ev, "split")) want = kEngineSplit;
-  }
-  if (want == kEngineSplit) {
-    if (!grid_ok) { set_error("split engine: working set exceeds 160 KiB LDS"); return GPT_ERR_BAD_DIMS; }
-    if (split_factor(nchains, (int)c->D, (int)c->m, device_cus()) < 2) {
-      set_error("split engine: D*S + 1 workgroups per chain (S >= 2) do not fit the GPU at once");
-      return GPT_ERR_BAD_DIMS;
+    else if (!std::strcmp(ev, "split")) {
+      set_error("the split engine (GPTSGLD_ENGINE=split) was removed"); return GPT_ERR_BAD_DIMS;
     }
+    else if (!std::strcmp(ev, "wave")) want = kEngineWave;
+  }
+  if (want == kEngineWave && !wave_ok) {
+    set_error("wave engine does not support this shape (needs SGLD+Stiefel, r in {6,8,10,12,15,"
+              "16,20}, 3r <= n <= 256, m <= 64, the V-phase working set within 160 KiB LDS)");
+    return GPT_ERR_BAD_DIMS;
   }
   if (want == kEngineChain && !chain_ok) {
     set_error("chain engine does not support this shape (needs D<=8, r<=5, n<=512 (even if >64), "
@@ -281,9 +271,10 @@ static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t 
   if (want == kEngineGrid && !grid_ok) {
     set_error("grid engine: working set exceeds 160 KiB LDS"); return GPT_ERR_BAD_DIMS;
   }
-  // few chains: the grid engine's D+1 workgroups per chain (the shorter step).  The split engine
-  // stays opt-in: its slices' exchange costs more than the batch work it divides at the
-  // measured shapes (scripts/single_chain.py)
+  // few chains: the grid engine's D+1 workgroups per chain (the shorter step)
+  // ranks past the chain engine: the wave engine (its step is shorter than the grid engine's even
+  // for one chain: the geodesic's expm runs on every dimension's wave at once)
+  if (want < 0 && !chain_ok && wave_ok) want = kEngineWave;
   if (want < 0 && grid_ok && (long long)nchains * (c->D + 1) <= device_cus()) want = kEngineGrid;
   *engine = want >= 0 ? want : (chain_ok ? kEngineChain : kEngineGrid);
   return GPT_OK;
@@ -332,6 +323,9 @@ static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t
   if (s->engine == kEngineChain)
     return launch_chain(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
                         t_local, nsteps, s->stream);
+  if (s->engine == kEngineWave)
+    return launch_wave(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
+                       t_local, false, s->stream);
   return launch_step(P, s->chains_d.as<ChainDesc>(), s->nchains, s->tbase.as<long long>(),
                      t_local, s->stream);
 }
@@ -339,8 +333,11 @@ static hipError_t session_launch(gpt_sgld_session* s, const StepParams& P, int t
 // temp of the first step (grid engine only: the chain engine forms temp inside its step).
 static int session_prime(gpt_sgld_session* s) {
   if (s->engine == kEngineChain || s->temp_ready) return GPT_OK;
-  hipError_t e = launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
-                                  s->tbase.as<long long>(), s->stream);
+  hipError_t e = s->engine == kEngineWave
+                     ? launch_wave(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
+                                   s->tbase.as<long long>(), 0, true, s->stream)
+                     : launch_temp_init(s->P, s->chains_d.as<ChainDesc>(), s->nchains,
+                                        s->tbase.as<long long>(), s->stream);
   if (e != hipSuccess) return hip_fail(e, "launch_temp_init");
   s->temp_ready = true;
   return GPT_OK;
@@ -435,8 +432,16 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     HIPCHK(hipMemcpy(s->runq.p, rq.data(), sizeof(int32_t) * rq.size(), hipMemcpyHostToDevice));
     P.runq = s->runq.as<int32_t>();
   }
+  P.wvtab = nullptr;
+  if (s->engine == kEngineWave) {
+    std::vector<int32_t> wt;
+    wave_tables(I0, Q, D, r, wt);
+    HIPCHK(s->wvtab.alloc(sizeof(int32_t) * wt.size()));
+    HIPCHK(hipMemcpy(s->wvtab.p, wt.data(), sizeof(int32_t) * wt.size(), hipMemcpyHostToDevice));
+    P.wvtab = s->wvtab.as<int32_t>();
+  }
   P.vtab = nullptr;
-  if (s->engine != kEngineChain && step_layout(n, D, r, Q, m).vcols) {
+  if (s->engine != kEngineChain && s->engine != kEngineWave && step_layout(n, D, r, Q, m).vcols) {
     std::vector<int32_t> vt;
     vphase_cols_tables(I0, n, D, r, Q, m, vt);
     HIPCHK(s->vtab.alloc(sizeof(int32_t) * vt.size()));
@@ -448,7 +453,6 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   P.rms = 0; P.rms_eps = 0.0; P.rms_alpha = 0.0;
   P.wonly = (store_flags & 16) ? 1 : 0;
   P.ncls = (store_flags & 32) ? nchains : 0;
-  P.split = s->engine == kEngineSplit ? split_factor(nchains, D, m, device_cus()) : 1;
   HIPCHK(s->tbase.alloc(sizeof(long long)));
   HIPCHK(hipMemset(s->tbase.p, 0, sizeof(long long)));
   HIPCHK(s->status.alloc(sizeof(int32_t) * nchains));
@@ -462,12 +466,12 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
                b_ws = s->store ? up(8 * (size_t)Q * s->nstore) : 0,
                b_Us = s->store ? up(8 * (size_t)n * r * D * s->nstore) : 0,
                b_dg = s->diag ? up(8 * (size_t)(1 + D) * s->total_steps) : 0,
-               b_sp = P.split > 1 ? up(8 * (size_t)D * P.split * n * r) + up(8 * (size_t)D) : 0;
+               b_wv = s->engine == kEngineWave ? up(8 * (size_t)D * m * r) + up(8 * (size_t)n * r * D) : 0;
   std::vector<double> w0(Q), U0((size_t)n * r * D);
   s->chains_h.resize(nchains);
   for (int c = 0; c < nchains; ++c) {
     std::unique_ptr<DevMem> mem(new DevMem());
-    HIPCHK(mem->alloc(b_w + b_U + b_temp + b_ord + b_ws + b_Us + b_dg + b_sp));
+    HIPCHK(mem->alloc(b_w + b_U + b_temp + b_ord + b_ws + b_Us + b_dg + b_wv));
     char* base = mem->as<char>();
     ChainDesc& C = s->chains_h[c];
     C.phi = phi_dev[c];
@@ -482,13 +486,11 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
     C.status = s->status.as<int32_t>() + c;
     C.seed = seeds[c];
     C.gw = C.gU = C.res = nullptr;
-    C.gpart = nullptr;
-    C.gcnt = nullptr;
-    if (b_sp) {
-      char* sp = base + b_w + b_U + b_temp + b_ord + b_ws + b_Us + b_dg;
-      C.gpart = (double*)sp;
-      C.gcnt = (unsigned long long*)(sp + up(8 * (size_t)D * P.split * n * r));
-      HIPCHK(hipMemset(C.gcnt, 0, 8 * (size_t)D));
+    C.coef = C.park = nullptr;
+    if (b_wv) {
+      char* wv = base + b_w + b_U + b_temp + b_ord + b_ws + b_Us + b_dg;
+      C.coef = (double*)wv;
+      C.park = (double*)(wv + up(8 * (size_t)D * m * r));
     }
     C.epsw = cfg->epsw; C.epsU = cfg->epsU; C.signal_var = cfg->signal_var; C.sigma_w = cfg->sigma_w;
     host_init_state(n, r, D, Q, seeds[c], cfg->stiefel != 0, cfg->sigma_w, w0.data(), U0.data());
@@ -722,8 +724,8 @@ extern "C" int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int6
     const int rc = session_prime(s);
     if (rc != GPT_OK) return rc;
   }
-  // one slot row per workgroup of a step: D+1 per chain, D·S+1 under the split engine
-  const size_t per = (size_t)(s->P.D * std::max(1, s->P.split) + 1) * s->nchains * kStamps;
+  // one slot row per workgroup of a step: D+1 per chain
+  const size_t per = (size_t)(s->P.D + 1) * s->nchains * kStamps;
   DevMem buf;
   HIPCHK(buf.alloc(8 * per * cnt));
   HIPCHK(hipMemset(buf.p, 0, 8 * per * cnt));
@@ -792,10 +794,14 @@ extern "C" int gpt_sgld_session_info(gpt_sgld_session* s, int64_t* out) {
     out[1] = (int64_t)chain_lds_bytes(P.n, P.D, P.r, P.Q, P.m);
     out[2] = 64 * P.D;
     out[3] = s->nchains;
+  } else if (s->engine == kEngineWave) {     // the dimension launch (the V-phase: one per chain)
+    out[1] = (int64_t)wv_dim_lds_bytes(P.n, P.r, P.m);
+    out[2] = 64;
+    out[3] = (int64_t)P.D * s->nchains;
   } else {
     out[1] = (int64_t)step_layout(P.n, P.D, P.r, P.Q, P.m).bytes;
     out[2] = kNT;
-    out[3] = (int64_t)(P.D * (P.split > 1 ? P.split : 1) + 1) * s->nchains;
+    out[3] = (int64_t)(P.D + 1) * s->nchains;
   }
   return GPT_OK;
 }
@@ -913,10 +919,6 @@ static int host_sampler(const gpt_sgld_config* cfg, const double* phi, const dou
   int32_t st = 0;
   rc = gpt_sgld_session_fetch(s, 0, w_store, U_store, diag, &st);
   if (rc != GPT_OK) return rc;
-  if (st == GPT_ERR_HIP) {                   // split engine: an in-kernel barrier timed out
-    set_error("split engine: the batch-slice barrier timed out (grid not resident)");
-    return GPT_ERR_HIP;
-  }
   if (st) {
     set_error("Get NaN when moving along Geodesic. Try smaller epsU");
     return GPT_ERR_NAN_GEODESIC;

@@ -21,8 +21,8 @@ constexpr int kNW = kNT / 64;      // waves per workgroup
 constexpr int kDMax = 16;          // max input dimensions D handled by the kernels
 constexpr int kEngineGrid = 0;     // sgld.hip: grid (D+1, chains), two batch reads per step
 constexpr int kEngineChain = 1;    // chain.hip: one workgroup per chain, one batch read per step
-constexpr int kEngineSplit = 2;    // sgld.hip with P.split = S: grid (D·S + 1, chains), the batch
-                                   // in S slices per dimension (single-chain latency)
+constexpr int kEngineWave = 3;     // wave.hip: per step a V-phase workgroup per chain, then one
+                                   // wave per (chain, dimension) (ranks past the chain engine)
 
 // Per-chain device state.  All pointers are device pointers.
 struct ChainDesc {
@@ -42,9 +42,8 @@ struct ChainDesc {
   double* gw;            // RMSprop (GPT_SGLD.jl:1121): Q moving average of squared gradw
   double* gU;            //   n*r*D moving average of squared gradU
   double* res;           //   m residuals of the step (written by the w phase)
-  double* gpart;         // split engine: D·S partial gradU (n·r each, unscaled) of the batch
-                         //   slices, [(k·S + s)·r + l]·n + j
-  unsigned long long* gcnt;   // split engine: D arrival counters (S per step, never reset)
+  double* coef;          // wave engine: D*m*r core sums A[l,k,i]*res_i of the step, [(k*m + i)*r + l]
+  double* park;          //   n*r*D the Stiefel momentum while the geodesic's expm holds the registers
 };
 
 struct StepParams {
@@ -59,14 +58,14 @@ struct StepParams {
   const int32_t* vtab;            // grid engine, column-lane V-phase: per workgroup kind (k < D,
                                   // w block = D) and core entry q, 16 ints: 8 temp row offsets
                                   // and I[q, k] (vphase_cols_tables), or null (vphase_tile)
+  const int32_t* wvtab;           // wave engine: D*Q run members (q with I[q,k] = l, q order, runs
+                                  // in l order) then D*(r+1) run starts (wave_tables)
   long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
   long long* tline;               // chain engine: per-workgroup timeline (kTimeline per block) or null
   int rms;                        // 1: GPT_SGLDERM_RMSprop steps (grid engine, two launches)
   int wonly;                      // 1: GPT_SGLDERMw steps (w alone, U fixed; grid engine)
   int ncls;                       // >= 2: GPTclassification, chains are the classes of one
                                   // model (grid engine; ChainDesc.res = class fhat, .gU = gradU)
-  int split;                      // grid engine: S >= 2 workgroups per dimension, each on one
-                                  // slice of the minibatch (the split engine, kEngineSplit), else 1
   double rms_eps, rms_alpha;      // its epsilon and moving-average coefficient
 };
 constexpr int kStamps = 16;       // stamp slots per block
@@ -195,6 +194,15 @@ size_t chain_lds_bytes(int n, int D, int r, int Q, int m);
 // nsteps consecutive steps per launch (steps t .. t+nsteps-1 of one epoch at most)
 hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchains,
                         const long long* tbase, int t_local, int nsteps, hipStream_t st);
+
+// Wave engine (wave.hip): two launches per step (V-phase per chain, then a wave per dimension);
+// init = the first step's temp only.
+bool wave_supported(int n, int D, int r, int Q, int m, bool langevin, bool stiefel);
+void wave_tables(const std::vector<int32_t>& I0, int Q, int D, int r, std::vector<int32_t>& out);
+size_t wv_dim_lds_bytes(int n, int r, int m);
+size_t wv_vphase_lds_bytes(int D, int r, int Q, int m);
+hipError_t launch_wave(const StepParams& P, const ChainDesc* chains, int nchains,
+                       const long long* tbase, int t_local, bool init, hipStream_t st);
 
 
 hipError_t launch_pred_x(const double* w, const double* U, const int32_t* I0, const double* X,

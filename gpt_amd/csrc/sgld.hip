@@ -50,12 +50,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   const ChainDesc C = chains[blockIdx.y];
   // kbase = D: the RMSprop w phase (one workgroup); kbase = D + 1: the class-fhat pass of
   // GPTclassification (one workgroup per class, before the step launch).
-  // Split engine (P.split = S >= 2, kbase = 0): workgroup x < D·S is (k = x / S, slice x % S) of
-  // the minibatch; x = D·S is the w block.
-  const int S = (P.split > 1 && kbase == 0) ? P.split : 1;
-  const int k = S > 1 ? ((int)blockIdx.x < P.D * S ? (int)blockIdx.x / S : P.D)
-                      : (int)blockIdx.x + kbase;
-  const int sl = (S > 1 && k < P.D) ? (int)blockIdx.x - k * S : 0;
+  const int k = (int)blockIdx.x + kbase;
   const int tid = threadIdx.x, wv = uni(tid >> 6);
   const long long t = tbase[0] + t_local;
   if (t >= P.total_steps) return;
@@ -90,12 +85,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   const bool has_next = t1 < P.total_steps;
   const int B1 = has_next ? min(m, P.N - s1) : 0;
   const int32_t* ord1 = C.order + (size_t)((has_next ? e1 : e) & 1) * P.N + (has_next ? s1 : start);
-  // this workgroup's batch columns [r0, r0 + Bs) and next-batch columns [r0n, r0n + Bsn)
-  const bool sliced = S > 1 && k < D;
-  const int r0 = sliced ? (Bt * sl) / S : 0;
-  const int Bs = sliced ? (Bt * (sl + 1)) / S - r0 : Bt;
-  const int r0n = sliced ? (B1 * sl) / S : 0;
-  const int Bsn = sliced ? (B1 * (sl + 1)) / S - r0n : B1;
+  const int Bs = Bt, Bsn = B1;         // this workgroup's batch columns and next-batch columns
   // rows of the next batch this lane touches into L2 during the V-phase (P5 streams them at the
   // end of the step): lanes 0-31 / 32-63 of wave w cover rows 2(w + kNW·x) + {0, 1}
   int trow[kTouch];
@@ -104,14 +94,14 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
 #pragma unroll
     for (int x = 0; x < kTouch; ++x) {
       const int i = 2 * (wv + kNW * x) + ((tid & 63) >> 5);
-      trow[x] = gptr(ord1)[r0n + min(i, Bsn - 1)];   // past the slice: its last row again
+      trow[x] = gptr(ord1)[min(i, Bsn - 1)];         // past the batch: its last row again
     }
   }
   STAMP(0);
 
   // ---- P0: stage temp (this batch), I, w, batch rows and targets
   {
-    const double* tsrc = C.temp + (size_t)(t & 1) * D * R * m + r0;
+    const double* tsrc = C.temp + (size_t)(t & 1) * D * R * m;
     for (int o = tid; o < D * R * MP; o += kNT) {   // zero tail: unrolled reads run past Bs
       const int row = o / MP, i = o - row * MP;
       temp_l[o] = i < Bs ? gptr(tsrc)[row * m + i] : 0.0;
@@ -123,7 +113,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     const double* wsrc = C.w + (size_t)(((P.rms && k < D) ? t + 1 : t) & 1) * Q;
     for (int q = tid; q < Q; q += kNT) w_l[q] = gptr(wsrc)[q];
     for (int i = tid; i < Bs; i += kNT) {
-      const int row = gptr(ord)[r0 + i];
+      const int row = gptr(ord)[i];
       idx_l[i] = row;
       y_l[i] = gptr(C.y)[row];
     }
@@ -161,7 +151,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     if (vcols) {
       double* vred = (double*)(smem + L.o_vred);
       const int32_t* tab = (const int32_t*)(smem + L.o_vtab);
-      if (Bs <= 32 && GPT_VHALF) {        // a split slice or a small batch: two q per pass
+      if (Bs <= 32 && GPT_VHALF) {        // a small batch: two q per pass
         if (k < D) vphase_cols_half<R, true>(temp_l, tab, w_l, Q, Bs, vred, vout);
         else vphase_cols_half<R, false>(temp_l, tab, w_l, Q, Bs, vred, vout);
       } else if (k < D) {
@@ -384,57 +374,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
         for (int l = 0; l < R; ++l)
           acc[l] = fma(p[u], GPT_EXP_P2NOCOEF ? 1e-3 * (l + u) : coef_l[l * MP + i0 + u], acc[l]);
     }
-    if (S > 1) {                  // the slice's partial sums; summed over the slices below
-      if (jok) {
-#pragma unroll
-        for (int l = 0; l < R; ++l)   // agent-coherent store: written through this XCD's L2
-          __hip_atomic_store(C.gpart + ((size_t)(k * S + sl) * R + l) * n + j, acc[l],
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      continue;
-    }
     if (jok) drive(j, acc);
-  }
-  if (S > 1) {
-    // the S workgroups of dimension k meet here (all of the grid is resident: the engine is only
-    // chosen when D·S + 1 workgroups per chain fit the GPU at once); each then sums the S partial
-    // sums in slice order — the same doubles in every one of them — and runs the rest of the step
-    // redundantly (the same noise, the same Stiefel move), so no second launch is needed.
-    // The slices of one dimension sit on different XCDs (L2s).  The exchange uses agent-scope
-    // relaxed atomics for the partial sums, the counter and its polls — each access goes to the
-    // coherence point on its own — and orders them by waiting for the stores' completion
-    // (s_waitcnt) before the arrival: agent-scope release/acquire FENCES would instead write back
-    // and invalidate the whole L2 of the XCD (every poll), evicting the next batch's rows.
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (tid == 0) {
-      unsigned long long* cnt = C.gcnt + k;
-      __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long target = (unsigned long long)S * (unsigned long long)(t + 1);
-      long long spins = 0;
-      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1ll << 26)) {             // never expected: a barrier that cannot close
-          __hip_atomic_store(C.status, GPT_ERR_HIP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    for (int j0 = 0; j0 < n; j0 += kNT) {
-      const int j = j0 + tid;
-      if (j >= n) continue;
-      double acc[R];
-#pragma unroll
-      for (int l = 0; l < R; ++l) {
-        double a = 0.0;
-        for (int s2 = 0; s2 < S; ++s2)
-          a += __hip_atomic_load(C.gpart + ((size_t)(k * S + s2) * R + l) * n + j,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc[l] = a;
-      }
-      drive(j, acc);
-    }
   }
   if (C.diag) {
     const double tot = blk_sum(gn2, red);
@@ -666,7 +606,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   {
     double* Uk = C.U + (size_t)n * R * k;
     double* Us = (store && C.U_store) ? C.U_store + ((size_t)slot * D + k) * n * R : nullptr;
-    for (int o = tid; o < (sl == 0 ? R * n : 0); o += kNT) {   // split: slice 0 writes
+    for (int o = tid; o < R * n; o += kNT) {
       const int l = o / n, j = o - l * n;
       const double u = U_l[l * NS + j];
       gptr_w(Uk)[o] = u;
@@ -678,22 +618,22 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   if (has_next) {
     __syncthreads();
     STAMP(9);
-    double* tdst = C.temp + (size_t)(t1 & 1) * D * R * m + (size_t)k * R * m + r0n;
+    double* tdst = C.temp + (size_t)(t1 & 1) * D * R * m + (size_t)k * R * m;
     auto p5out = [&](int l, int i, double v) { gptr_w(tdst)[l * m + i] = v; };
     // the fewest batch columns per wave pass that cover the (slice of the) next batch in one pass
     // (fewer row loads, and at <= 32 values a half-size butterfly)
     if constexpr (RCfgX<R, 4>::ICH != RCfgX<R, 8>::ICH) {
       if (Bsn <= kNW * RCfgX<R, 4>::ICH) {
-        phidotU_tile<R, decltype(p5out), 4>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS,
+        phidotU_tile<R, decltype(p5out), 4>(C.phi, koff, rstride, ord1, 0, Bsn, n, NP, NS,
                                             U_l, p5out);
       } else if (Bsn <= kNW * RCfgX<R, 7>::ICH) {
-        phidotU_tile<R, decltype(p5out), 7>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS,
+        phidotU_tile<R, decltype(p5out), 7>(C.phi, koff, rstride, ord1, 0, Bsn, n, NP, NS,
                                             U_l, p5out);
       } else {
-        phidotU_tile<R>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS, U_l, p5out);
+        phidotU_tile<R>(C.phi, koff, rstride, ord1, 0, Bsn, n, NP, NS, U_l, p5out);
       }
     } else {
-      phidotU_tile<R>(C.phi, koff, rstride, ord1 + r0n, 0, Bsn, n, NP, NS, U_l, p5out);
+      phidotU_tile<R>(C.phi, koff, rstride, ord1, 0, Bsn, n, NP, NS, U_l, p5out);
     }
     __syncthreads();
     STAMP(10);
@@ -784,7 +724,7 @@ hipError_t launch_temp_init(const StepParams& P, const ChainDesc* chains, int nc
 hipError_t launch_step(const StepParams& P, const ChainDesc* chains, int nchains,
                        const long long* tbase, int t_local, hipStream_t st) {
   const StepLayout L = step_layout(P.n, P.D, P.r, P.Q, P.m);
-  dim3 grid(P.D * (P.split > 1 ? P.split : 1) + 1, nchains);
+  dim3 grid(P.D + 1, nchains);
   switch (P.r) {
 #define CASE(RR)                                                                              \
   case RR:                                                                                    \

@@ -15,8 +15,8 @@ from .GPT_SGLD import make_config
 
 
 # store_flags bits selecting the step engine (include/gptsgld.h, gpt_sgld_session_info)
-ENGINES = {"auto": 0, "grid": 4, "chain": 8, "split": 64}
-ENGINE_NAMES = {0: "grid", 1: "chain", 2: "split"}
+ENGINES = {"auto": 0, "grid": 4, "chain": 8, "wave": 128}
+ENGINE_NAMES = {0: "grid", 1: "chain", 3: "wave"}
 
 
 class SGLDSession:
@@ -114,8 +114,7 @@ class SGLDSession:
                                                   C.c_void_p(U_out.data_ptr())))
 
     def status(self, chain):
-        """GPT_OK, GPT_ERR_NAN_GEODESIC when chain hit the geodesic bail-out, or GPT_ERR_HIP when a
-        split-engine barrier timed out (4 bytes copied)."""
+        """GPT_OK, or GPT_ERR_NAN_GEODESIC when chain hit the geodesic bail-out (4 bytes copied)."""
         st = C.c_int32(0)
         check(lib().gpt_sgld_session_fetch(self._h, chain, None, None, None, C.byref(st)))
         return st.value

@@ -151,7 +151,7 @@ int64_t gpt_sgld_session_steps_done(gpt_sgld_session* s);
 int gpt_sgld_session_time_steps(gpt_sgld_session* s, int64_t nsteps, double* avg_us);
 /* Diagnostic: run nsteps un-captured steps recording s_memtime (shader-clock ticks)
  * stamps per phase; out = nsteps x W x 16 int64 (0 = phase not reached), W = the workgroups of
- * one step ((D+1)*nchains; (D*S+1)*nchains under the split engine, gpt_sgld_session_info). */
+ * one step ((D+1)*nchains, grid engine; gpt_sgld_session_info). */
 int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out);
 /* Diagnostic (chain engine): ONE launch of nsteps steps (within the current epoch, <= 512);
  * out = nchains x gpt_sgld_timeline_slots() int64: per block {s_memrealtime, s_memtime} at slot
@@ -160,20 +160,22 @@ int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out);
  * *event_us = the launch's hipEvent time. */
 int64_t gpt_sgld_timeline_slots(void);
 int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, int64_t* out, double* event_us);
-/* Copy chain c's stores / status back (status: GPT_OK, GPT_ERR_NAN_GEODESIC, or GPT_ERR_HIP when a
- * split-engine batch-slice barrier timed out; stores are zero-filled for a non-zero status). */
+/* Copy chain c's stores / status back (status: GPT_OK or GPT_ERR_NAN_GEODESIC; stores are
+ * zero-filled for a non-zero status). */
 int gpt_sgld_session_fetch(gpt_sgld_session* s, int32_t chain, double* w_store, double* U_store,
                            double* diag, int32_t* status);
 void gpt_sgld_session_destroy(gpt_sgld_session* s);
-/* out[4] = {engine (0 grid: D+1 workgroups per chain, 1 chain: one workgroup per chain),
- *           LDS bytes per workgroup, threads per workgroup, workgroups per step launch}.
+/* out[4] = {engine, LDS bytes per workgroup, threads per workgroup, workgroups per step launch}.
+ * Engines: 0 grid (sgld.hip: D+1 workgroups per chain, one step per launch), 1 chain (chain.hip:
+ * one workgroup per chain, up to an epoch of steps per launch; r <= 5), 3 wave (wave.hip: per
+ * step a V-phase workgroup per chain, then one wave per (chain, dimension); the figures are the
+ * dimension launch's).  Engine 2 (the round-3 split engine) was removed.
  * store_flags of gpt_sgld_session_create: bit0 stores, bit1 diagnostics, bit2 force the grid
- * engine, bit3 force the chain engine, bit6 force the split engine (engine 2: the grid engine
- * with the minibatch in S >= 2 slices per dimension, D*S + 1 workgroups per chain, one in-kernel
- * barrier per step).  Default: the split engine while nchains*(D*S+1) workgroups fit the GPU's
- * CUs for some S >= 2 (the shortest step), else the grid engine while nchains*(D+1) do, else the
- * chain engine whenever the shape allows it; GPTSGLD_ENGINE=grid|chain|split overrides the
- * default and GPTSGLD_SPLIT=S the slice count. */
+ * engine, bit3 force the chain engine, bit7 force the wave engine (bit6, the split engine, is
+ * rejected).  Default: the chain engine whenever the shape allows it (few chains: the grid engine
+ * while nchains*(D+1) workgroups fit the GPU's CUs), else the wave engine whenever the shape
+ * allows it (SGLD + Stiefel, r in {6,8,10,12,15,16,20}, 3r <= n <= 256, m <= 64), else the grid
+ * engine; GPTSGLD_ENGINE=grid|chain|wave overrides the default. */
 int gpt_sgld_session_info(gpt_sgld_session* s, int64_t* out);
 
 /* ---- prediction ---------------------------------------------------------------------- */

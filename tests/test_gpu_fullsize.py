@@ -115,3 +115,75 @@ def test_fullsize_chain_matches_oracle_and_single_runs(problem):
         want = R.pred(wn[c], Uc, problem["I"], phi_te_np)
         assert rel(fh[c], want) < 1e-12
     s.close()
+
+
+def _gram_err(s, C, n_, r_, D_):
+    import torch
+    w_all = torch.empty((C, Q), dtype=torch.float64, device="cuda")
+    U_all = torch.empty((C, n_ * r_ * D_), dtype=torch.float64, device="cuda")
+    s.gather_state(0, C, w_all, U_all)
+    s.sync()
+    Ut = U_all.view(C, D_, r_, n_)
+    gram = torch.einsum("ckaj,ckbj->ckab", Ut, Ut)
+    eye = torch.eye(r_, dtype=torch.float64, device="cuda")
+    return (gram - eye).abs().amax(dim=(1, 2, 3)).cpu().numpy()
+
+
+def test_fullsize_chain_stiefel_invariant_200_epochs(problem):
+    """The bench's launch (256 chains, chain engine) over the reference's 200 epochs (40 000
+    steps): every chain stays on the manifold (max |UᵀU − I| <= 1e-10 per dimension), the
+    precondition of the kernel's A = (M − Mᵀ)/2 (GPT_SGLD.jl:21 replaced, chain.hip)."""
+    from gpt_amd.session import SGLDSession
+    nb = -(-problem["ytr"].size // m)
+    s = SGLDSession(problem["phi"], problem["y"], problem["I"], r, Q, m, EPSW, EPSU, SV, 0, 200,
+                    list(range(1, 257)), store=False, engine="chain")
+    s.run(200 * nb)
+    s.sync()
+    assert all(s.status(c) == 0 for c in range(256))
+    err = _gram_err(s, 256, n, r, D)
+    s.close()
+    assert err.max() <= 1e-10, err.max()
+
+
+def test_r20_wave_stiefel_invariant_and_independence():
+    """kin40kExperiment.jl's shape (n = 150, r = 20, εw = 1e-4, εU = 1e-7) on the wave engine with
+    256 chains for 20 epochs (4 000 steps): surviving chains stay on the manifold (<= 1e-10),
+    and chain 0 equals a one-chain session of its seed bit for bit."""
+    import torch
+    import bench
+    from gpt_amd import GPT_SGLD as G
+    from gpt_amd.session import SGLDSession, feature_device
+    n2, r2 = 150, 20
+    Xtr, ytr, _, _, _ = bench.kin40k(D)
+    ls = np.array([2.5242, 2.3376, 1.3630, 1.4949, 1.6022, 1.1366, 1.1964, 1.7028])
+    I = G.samplenz(r2, D, Q, 17)
+    Z, b = G.feature_inputs(n2, D, 17)
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    phi = feature_device(tt(Xtr.T), tt(ls), 1.0420, math.sqrt(n2 / Q ** (1.0 / D)), tt(Z.T), tt(b.T))
+    y = tt(ytr)
+    nb = -(-ytr.size // m)
+    s = SGLDSession(phi, y, I, r2, Q, m, 1e-4, 1e-7, SV, 0, 20, list(range(1, 257)), store=False,
+                    engine="wave")
+    s.run(20 * nb)
+    s.sync()
+    alive = [c for c in range(256) if s.status(c) == 0]
+    assert len(alive) >= 128, len(alive)
+    err = _gram_err(s, 256, n2, r2, D)
+    U_all = torch.empty((1, n2 * r2 * D), dtype=torch.float64, device="cuda")
+    w_all = torch.empty((1, Q), dtype=torch.float64, device="cuda")
+    s.gather_state(0, 1, w_all, U_all)
+    s.sync()
+    s.close()
+    assert err[alive].max() <= 1e-10, err[alive].max()
+    s1 = SGLDSession(phi, y, I, r2, Q, m, 1e-4, 1e-7, SV, 0, 20, [1], store=False, engine="wave")
+    s1.run(20 * nb)
+    s1.sync()
+    U1 = torch.empty_like(U_all)
+    w1 = torch.empty_like(w_all)
+    s1.gather_state(0, 1, w1, U1)
+    s1.sync()
+    st = s1.status(0)
+    s1.close()
+    if 0 in alive:
+        assert st == 0
+        assert torch.equal(U1, U_all) and torch.equal(w1, w_all)

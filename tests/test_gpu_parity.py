@@ -193,6 +193,15 @@ CASES = {
     # more than 8 input dimensions: the grid engine's lane-per-q V-phase tile (the column-lane
     # form and the chain engine stop at D = 8), split into slices of 7 / 8 rows
     "d12": (40, 12, 80, 2, 24, 15, 0, 2, 1, True, True),
+    # wave engine shapes (wave.hip, r > 5): one 64-row block, ragged thinned batches after burn-in,
+    # four row blocks (J = 4), odd n with odd 2r, the 2r = 32 one-pass solve at the m = 64 maximum,
+    # 12 input dimensions at r = 20
+    "w_r6_d3": (40, 3, 70, 6, 30, 16, 0, 2, 1, True, True),
+    "w_r8_thin": (96, 4, 55, 8, 50, 12, 1, 2, 3, True, True),
+    "w_r12_n200": (200, 5, 64, 12, 100, 32, 0, 1, 1, True, True),
+    "w_r15_odd": (77, 6, 40, 15, 90, 9, 0, 2, 1, True, True),
+    "w_r16_m64": (130, 4, 130, 16, 120, 64, 0, 1, 1, True, True),
+    "w_r20_d12": (64, 12, 30, 20, 60, 10, 0, 1, 1, True, True),
 }
 
 
@@ -205,15 +214,20 @@ def _shape(name):
     return [CASES[name][i] for i in (0, 1, 3, 9, 10)]
 
 
-def _split_ok(name):
-    """The split engine takes a batch of >= 12 rows (two slices of 6) and any shape the grid
-    engine takes."""
-    return CASES[name][5] >= 12
+WAVE_RANKS = (6, 8, 10, 12, 15, 16, 20)
 
 
-ENGINE_CASES = [(name, eng) for name in CASES for eng in ("grid", "chain", "split")
-                if eng == "grid" or (eng == "chain" and _chain_ok(*_shape(name)))
-                or (eng == "split" and _split_ok(name))]
+def _wave_ok(name):
+    """Shapes the wave engine (wave.hip) takes: SGLD + Stiefel at an instantiated r > 5,
+    3r <= n <= 256, m <= 64."""
+    n, D, N, r, Q, m, burnin, maxepoch, se, lang, stf = CASES[name]
+    return lang and stf and r in WAVE_RANKS and 3 * r <= n <= 256 and m <= 64
+
+
+ENGINE_CASES = [(name, eng) for name in CASES for eng in ("grid", "chain", "wave")
+                if (eng == "grid" and not name.startswith("w_"))
+                or (eng == "chain" and _chain_ok(*_shape(name)))
+                or (eng == "wave" and _wave_ok(name))]
 
 
 @pytest.mark.parametrize("name,engine", ENGINE_CASES)
@@ -437,9 +451,9 @@ def test_sgldERM_generation_a_mapping():
     assert rel(ws, wo) < 1e-8 and rel(Us, Uo) < 1e-8
 
 
-@pytest.mark.parametrize("engine", ["grid", "chain"])
+@pytest.mark.parametrize("engine", ["grid", "chain", "wave"])
 def test_injected_initial_state(engine):
-    n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
+    n, D, N, r, Q, m = (12, 3, 30, 2, 6, 10) if engine != "wave" else (24, 3, 30, 6, 6, 10)
     p = make_problem(n, D, N, r, Q, seed=8)
     rng = np.random.default_rng(0)
     w0 = rng.standard_normal(Q)
@@ -451,9 +465,9 @@ def test_injected_initial_state(engine):
     assert rel(ws, wo) < 1e-8 and rel(Us, Uo) < 1e-8
 
 
-@pytest.mark.parametrize("engine", ["grid", "chain"])
+@pytest.mark.parametrize("engine", ["grid", "chain", "wave"])
 def test_nan_geodesic_bailout_zero_fills(capsys, engine):
-    n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
+    n, D, N, r, Q, m = (12, 3, 30, 2, 6, 10) if engine != "wave" else (24, 3, 30, 6, 6, 10)
     p = make_problem(n, D, N, r, Q, seed=6)
     ws, Us = G().GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e300, 0, 2, 3,
                                engine=engine)
@@ -484,11 +498,11 @@ def test_gpnt_sgld_matches_oracle():
     assert rel(got, want) < 1e-9
 
 
-@pytest.mark.parametrize("engine", ["grid", "chain", "split"])
+@pytest.mark.parametrize("engine", ["grid", "chain", "wave"])
 def test_multichain_session_equals_single_runs(engine):
     import torch
     from gpt_amd.session import SGLDSession
-    n, D, N, r, Q, m = 32, 4, 60, 3, 12, 16
+    n, D, N, r, Q, m = (32, 4, 60, 3, 12, 16) if engine != "wave" else (32, 4, 60, 6, 12, 16)
     p = make_problem(n, D, N, r, Q, seed=21)
     phi_t = torch.from_numpy(np.ascontiguousarray(p["phi"].transpose(2, 1, 0))).cuda()
     y_t = torch.from_numpy(p["y"]).cuda()
@@ -509,12 +523,12 @@ def test_multichain_session_equals_single_runs(engine):
     s.close()
 
 
-@pytest.mark.parametrize("engine", ["grid", "chain"])
+@pytest.mark.parametrize("engine", ["grid", "chain", "wave"])
 def test_epoch_order_ring_over_many_epochs(engine):
     """Seven epochs of a ragged N (nb = 4) with every epoch-end sample stored: the two-slot order
     ring (order.hip) must hand each epoch its own composed permutation, through direct launches
     and graph replays alike."""
-    n, D, N, r, Q, m = 24, 3, 29, 3, 10, 8
+    n, D, N, r, Q, m = (24, 3, 29, 3, 10, 8) if engine != "wave" else (24, 3, 29, 6, 10, 8)
     p = make_problem(n, D, N, r, Q, seed=31)
     got_w, got_U = G().GPTregression(p["phi"], p["y"], 0.05, p["I"], r, Q, m, 1e-4, 1e-6, 1, 6, 9,
                                      store_every=2, engine=engine)
@@ -524,47 +538,40 @@ def test_epoch_order_ring_over_many_epochs(engine):
     assert rel(got_w, wo) < 1e-8 and rel(got_U, Uo) < 1e-8
 
 
-@pytest.mark.parametrize("name,S", [("last_row_alone", 4), ("small", 8), ("ragged_thin", 3),
-                                    ("kin40k_shape", 2)])
-def test_split_engine_slices_match_oracle(name, S, monkeypatch):
-    """The split engine with S forced (GPTSGLD_SPLIT): slices of one row, empty slices of a
-    last batch of one row, ragged slices — the same trajectories as the oracle (the partial
-    gradU sums of the slices add up in slice order, a different rounding than one sum)."""
-    monkeypatch.setenv("GPTSGLD_SPLIT", str(S))
-    n, D, N, r, Q, m, burnin, maxepoch, se, lang, stf = CASES[name]
-    p = make_problem(n, D, N, r, Q, seed=11)
-    epsw, epsU, sv, seed = 1e-4, 1e-6, 0.05, 23
-    ws, Us, dg = G().GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
-                                   maxepoch, seed, diag=True, langevin=lang, stiefel=stf,
-                                   store_every=se, engine="split")
-    wo, Uo, info = R.GPTregression(p["phi"], p["y"], sv, p["I"], r, Q, m, epsw, epsU, burnin,
-                                   maxepoch, seed, record=True, langevin=lang, stiefel=stf,
-                                   store_every=se)
-    assert info["status"] == 0
-    assert rel(ws, wo) < 1e-8, rel(ws, wo)
-    assert rel(Us, Uo) < 1e-8, rel(Us, Uo)
-    assert rel(dg[1:], np.array(info["gradU_norm"]).T) < 1e-9
-
-
-def test_single_chain_default_and_split_opt_in():
-    """One chain at the kin40k shape: the library picks the grid engine (D + 1 workgroups, the
-    shorter step, scripts/single_chain.py); the split engine is opt-in and runs D·S + 1."""
+def test_engine_selection():
+    """One chain at the kin40k shape runs the grid engine (D + 1 workgroups, the shorter step);
+    r = 20 at the reference's kin40k shape runs the wave engine by default; the removed split
+    engine is rejected."""
     import torch
+    from gpt_amd._lib import GPTError
     from gpt_amd.session import SGLDSession
-    n, D, N, r, Q, m = 500, 8, 200, 5, 200, 50
-    p = make_problem(n, D, N, r, Q, seed=3)
     dev = torch.device("cuda", 0)
-    phi = torch.from_numpy(np.ascontiguousarray(np.asarray(p["phi"]).transpose(2, 1, 0))).to(dev)
-    y = torch.from_numpy(np.ascontiguousarray(np.asarray(p["y"], dtype=np.float64))).to(dev)
-    s = SGLDSession(phi, y, p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 1, [5])
-    info = s.info()
-    s.close()
-    assert info["engine"] == "grid" and info["workgroups"] == D + 1
-    s = SGLDSession(phi, y, p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 1, [5], engine="split")
-    info = s.info()
-    s.close()
-    assert info["engine"] == "split" and (info["workgroups"] - 1) % D == 0
-    assert info["workgroups"] > D + 1
+    for (n, D, N, r, Q, m), want in [((500, 8, 200, 5, 200, 50), "grid"),
+                                     ((150, 8, 100, 20, 200, 50), "wave")]:
+        p = make_problem(n, D, N, r, Q, seed=3)
+        phi = torch.from_numpy(np.ascontiguousarray(np.asarray(p["phi"]).transpose(2, 1, 0))).to(dev)
+        y = torch.from_numpy(np.ascontiguousarray(np.asarray(p["y"], dtype=np.float64))).to(dev)
+        s = SGLDSession(phi, y, p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 1, [5])
+        info = s.info()
+        s.close()
+        assert info["engine"] == want
+        if want == "grid":
+            assert info["workgroups"] == D + 1
+        else:
+            assert info["workgroups"] == D and info["threads"] == 64
+    with pytest.raises(GPTError):
+        import ctypes as C
+        from gpt_amd import _lib
+        from gpt_amd.GPT_SGLD import make_config
+        cfg = make_config(16, 3, 40, 2, 6, 8, 1e-4, 1e-6, 0.05, 1.0, 0, 1, 0, True, True, 1, 0)
+        p = make_problem(16, 3, 40, 2, 6, seed=1)
+        phi = torch.from_numpy(np.ascontiguousarray(np.asarray(p["phi"]).transpose(2, 1, 0))).to(dev)
+        y = torch.from_numpy(np.ascontiguousarray(np.asarray(p["y"], dtype=np.float64))).to(dev)
+        I = np.asfortranarray(np.asarray(p["I"], dtype=np.int32))
+        h = C.c_void_p()
+        _lib.check(_lib.lib().gpt_sgld_session_create(
+            C.byref(cfg), 1, (C.c_uint64 * 1)(1), (C.c_void_p * 1)(phi.data_ptr()),
+            (C.c_void_p * 1)(y.data_ptr()), I.ctypes.data_as(_lib.P_I32), 1 | 64, None, C.byref(h)))
 
 
 def test_chain_engine_declines_odd_n_past_one_block():

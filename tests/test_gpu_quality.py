@@ -50,6 +50,25 @@ def rel(a, b):
     return np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
 
 
+def stiefel_errors(sess, chains, n, r, D):
+    """max_k |U_kᵀU_k − I| of the current U of each chain (device state, gathered).  The step
+    kernels take geod's A = Uᵀmom as (M − Mᵀ)/2 from the projection's M = UᵀW (chain and wave
+    engines) and the grid engine S from the same identity (GPT_SGLD.jl:19-22 replaced): both hold
+    only on the manifold, so the invariant is asserted after the long runs that rely on them."""
+    import torch
+    dev = torch.device("cuda", 0)
+    out = []
+    for c in chains:
+        w_t = torch.empty((1, sess.Q), dtype=torch.float64, device=dev)
+        U_t = torch.empty((1, n * r * D), dtype=torch.float64, device=dev)
+        sess.gather_state(c, 1, w_t, U_t)
+        sess.sync()
+        U = U_t.cpu().numpy().reshape((D, r, n)).transpose(2, 1, 0)      # Julia (n, r, D)
+        out.append(max(float(np.abs(U[:, :, k].T @ U[:, :, k] - np.eye(r)).max())
+                       for k in range(D)))
+    return out
+
+
 def test_kin40k_reference_configuration_tracks_reference_curve():
     """kin40kExperiment.jl:38-91 over its full 200 epochs (10 sweeps, r = 20, n = 150) against
     testRMSE_kin40k.h5: bands in the assertions below."""
@@ -77,8 +96,11 @@ def test_kin40k_reference_configuration_tracks_reference_curve():
         phites.append(feature_device(Xte_d, tt(ls), srbf, scale, Z_d, b_d))
     sess = SGLDSession(phis, tt(ytr), I, r, Q, m, 1e-4, 1e-7, 0.0476, 0, epochs,
                        list(range(1, sweeps + 1)), store_every=nb, store=True)
+    engine = sess.info()["engine"]
     sess.run(epochs * nb)
     sess.sync()
+    alive_c = [c for c in range(sweeps) if sess.status(c) == 0]
+    st_err = stiefel_errors(sess, alive_c, n, r, D)
     I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
     yte_d = tt(yte)
     fh = torch.empty((epochs, Nte), dtype=torch.float64, device=dev)
@@ -95,9 +117,12 @@ def test_kin40k_reference_configuration_tracks_reference_curve():
         curves.append((ysd * torch.sqrt((err * err).mean(dim=1))).cpu().numpy())   # :83
     sess.close()
     assert alive >= 6, "only %d of %d sweeps survived" % (alive, sweeps)
+    # the manifold invariant behind the kernels' Gram identities, after 40 000 steps
+    assert max(st_err) <= 1e-10, st_err
     curves = np.array(curves)
     final, last50 = curves[:, -1], curves[:, -50:].mean(axis=1)
     _record("kin40k_reference_config", dict(
+        engine=engine, stiefel_err=st_err,
         sweeps=sweeps, survived=alive, epochs=epochs, final=final.tolist(),
         last50_curve_mean=last50.tolist(), median_final=float(np.median(final)),
         median_last50=float(np.median(last50)), ref_final=float(ref[-1]),
@@ -202,6 +227,9 @@ def _pp_curves(seeds, epochs, epsw, epsU, rms=None, m=256):
         sess.set_rmsprop(*rms)
     sess.run(epochs * nb)
     sess.sync()
+    alive_c = [c for c in range(len(seeds)) if sess.status(c) == 0]
+    st_err = stiefel_errors(sess, alive_c, n, r, D)
+    assert max(st_err) <= 1e-10, st_err            # the manifold invariant after 4 000 steps
     I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
     yte_d = tt(yte)
     fh = torch.empty((epochs, Nte), dtype=torch.float64, device=dev)
