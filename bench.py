@@ -52,13 +52,30 @@ def powerplant(D, ntrain=5000):
     return (Xtr - mu) / sd, (ytr - ymu) / ysd, (Xte - mu) / sd, (yte - ymu) / ysd, ysd
 
 
+KIN40K_LS = [2.5242, 2.3376, 1.3630, 1.4949, 1.6022, 1.1366, 1.1964, 1.7028]
 WORKLOADS = {
-    # name: (loader, D, minibatch, length scales, sigma_RBF, signal_var, description)
-    "kin40k": (kin40k, 8, 50, [2.5242, 2.3376, 1.3630, 1.4949, 1.6022, 1.1366, 1.1964, 1.7028],
-               1.0420, 0.0476, "kin40k tensor-GP SGLD (GPTregression)"),
+    # name: (loader, D, minibatch, length scales, sigma_RBF, signal_var, description,
+    #        defaults n, r, epsw, epsU)
+    "kin40k": (kin40k, 8, 50, KIN40K_LS, 1.0420, 0.0476, "kin40k tensor-GP SGLD (GPTregression)",
+               500, 5, 1e-5, 1e-8),
+    # the configuration kin40kExperiment.jl itself runs (:38-51: n = 150, r = 20, Q = 200, m = 50,
+    # εw = 1e-4, εU = 1e-7) — the only kin40k shape with a reference test-RMSE curve
+    # (testRMSE_kin40k.h5): the wave engine (wave.hip)
+    "kin40k_ref": (kin40k, 8, 50, KIN40K_LS, 1.0420, 0.0476,
+                   "kin40k tensor-GP SGLD at kin40kExperiment.jl's configuration (GPTregression)",
+                   150, 20, 1e-4, 1e-7),
+    # εw = 5e-5, εU = 2e-8: the round-4 oracle sweep's best stable pair at this shape
+    # (scripts/pp_step_sweep.py; tests/test_gpu_quality.py)
     "powerplant": (powerplant, 4, 256, [1.4332] * 4, 1.0, 0.2299 ** 2,
-                   "PowerPlant tensor-GP SGLD (GPTregression), BASELINE config 2"),
+                   "PowerPlant tensor-GP SGLD (GPTregression), BASELINE config 2", 500, 5, 5e-5, 2e-8),
 }
+METRICS = {
+    "kin40k": "SGLD steps/sec (kin40k, n_feat=500/dim, r=5)",
+    "kin40k_ref": "SGLD steps/sec + test RMSE (kin40kExperiment.jl: n_feat=150/dim, r=20, m=50)",
+    "powerplant": "SGLD steps/sec (PowerPlant, n_feat=500/dim, r=5, minibatch 256)",
+}
+KERNELS = {"chain": "chain_kernel<%d,J,2>", "grid": "sgld_step_kernel<%d>",
+           "wave": "wv_vphase_kernel<%d> + wv_dim_kernel<%d,J>"}
 
 
 def algorithmic_bytes_per_step(n, D, B, r, Q):
@@ -67,7 +84,20 @@ def algorithmic_bytes_per_step(n, D, B, r, Q):
 
 
 def algorithmic_flops_per_step(n, D, B, r, Q):
+    """4nrDB + 3QDB + 4QB + D(14nr² + 2·30·(2r)³) flops per SGLD step (the last
+    term prices geod's two expm at 30 (2r)³-products, a generous Padé count)."""
     return 4 * n * r * D * B + 3 * Q * D * B + 4 * Q * B + D * (14 * n * r * r + 2 * 30 * (2 * r) ** 3)
+
+
+def executed_flops_per_step(n, D, B, r, Q):
+    """The flops the wave engine executes per step at the Padé degree the kin40k runs take (5: three
+    2r x 2r products, a 2r x 2r LU with 2r right-hand sides; the r x r expm likewise), for
+    comparison with the §8(d) count: phidotU + gradU 4nrDB, V / A 3QDB, fhat / gradw 4QB, proj +
+    Grams + tmpU D·(2nr² · 5 + 2·2nr·r), the expm D·(3·2(2r)³ + (8/3)(2r)³ + 3·2r³ + (8/3)r³)."""
+    nn = 2 * r
+    expm = 3 * 2 * nn ** 3 + 8 * nn ** 3 / 3 + 3 * 2 * r ** 3 + 8 * r ** 3 / 3
+    return (4 * n * r * D * B + 3 * Q * D * B + 4 * Q * B
+            + D * (2 * n * r * r * 5 + 2 * 2 * n * r * r + expm))
 
 
 def _cpu_threads():
@@ -222,8 +252,7 @@ def compose_line(v):
     pred_tfs = v.pred_flop / (v.pred_ms * 1e-3) / 1e12
     gemm_tfs = v.pred_flop / (v.gemm_ms * 1e-3) / 1e12
     return {
-        "metric": ("SGLD steps/sec (kin40k, n_feat=500/dim, r=5)" if a.workload == "kin40k"
-                   else "SGLD steps/sec (PowerPlant, n_feat=500/dim, r=5, minibatch 256)"),
+        "metric": METRICS[a.workload],
         "value": v.value,
         "unit": "chain-steps/s",
         "n_gpus": v.world,
@@ -244,18 +273,17 @@ def compose_line(v):
                    "signal_var": a.signal_var, "parallelism": "chains%dx%d" % (v.C, v.world),
                    "engine": v.info["engine"], "workgroups_per_launch": v.info["workgroups"],
                    "threads_per_workgroup": v.info["threads"], "lds_bytes": v.info["lds_bytes"]},
-        "roofline": {"bound": "hbm", "achieved": v.achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": v.achieved / HBM_PEAK_GBS, "traffic": v.traffic,
-                     "traffic_source": v.traffic_src,
-                     "kernel": ("chain_kernel<%d,J,2>" if v.info["engine"] == "chain"
-                                else "sgld_step_kernel<%d>") % v.r, "kernel_us": v.k_us,
+        "roofline": dict(v.roof, **{
+                     "traffic": v.traffic, "traffic_source": v.traffic_src,
+                     "kernel": KERNELS[v.info["engine"]].replace("%d", str(v.r)),
+                     "kernel_us": v.k_us,
                      "kernel_us_per_rank": v.k_us_ranks,
                      "kernel_us_note": "per step of all chains; the chain engine runs up to "
                                        "one epoch of steps per launch (one event pair per "
                                        "launch, total / steps)",
                      "algorithmic_bytes_per_launch": v.bytes_launch,
                      "algorithmic_bytes_per_step": v.bytes_launch,
-                     "steps_run_per_chain": v.steps_run},
+                     "steps_run_per_chain": v.steps_run}),
         "cpu_baseline": v.cpu,
         "test_rmse": v.quality["test_rmse"],
         "test_rmse_note": v.quality["note"],
@@ -296,19 +324,19 @@ def main():
     ap.add_argument("--chains", type=int, default=0,
                     help="independent chains per GPU (0: one per CU for the chain engine, two at "
                          "D <= 4; CUs // (D+1) for the grid engine, D+1 workgroups per chain)")
-    ap.add_argument("--engine", default="auto", choices=["auto", "grid", "chain"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "grid", "chain", "wave"])
     ap.add_argument("--workload", default="kin40k", choices=sorted(WORKLOADS),
                     help="kin40k (BASELINE configs 3/4, the metric's workload) or powerplant (config 2)")
-    ap.add_argument("--n", type=int, default=500)
+    ap.add_argument("--n", type=int, default=None, help="default: the workload's (500 / 150)")
     ap.add_argument("--D", type=int, default=None, help="default: the workload's D (8 / 4)")
-    ap.add_argument("--r", type=int, default=5)
+    ap.add_argument("--r", type=int, default=None, help="default: the workload's (5 / 20)")
     ap.add_argument("--Q", type=int, default=200)
     ap.add_argument("--m", type=int, default=None, help="minibatch (default: 50 / 256)")
     # kin40kExperiment.jl:50-51 uses εw=1e-4, εU=1e-7 at n=150, r=20; under the restated
     # GPT_SGLD.jl update both the oracle and the GPU path diverge there (w Hessian λmax≈3e5),
     # so the benchmark uses the largest stable pair found by the oracle sweep.
-    ap.add_argument("--epsw", type=float, default=1e-5)
-    ap.add_argument("--epsU", type=float, default=1e-8)
+    ap.add_argument("--epsw", type=float, default=None, help="default: the workload's")
+    ap.add_argument("--epsU", type=float, default=None, help="default: the workload's")
     ap.add_argument("--signal_var", type=float, default=None, help="default: the workload's")
     ap.add_argument("--kernel-steps", type=int, default=100, help="steps of the event-timed pass")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -327,7 +355,10 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: re-run under torchrun before any HIP call in this process
         raise SystemExit(self_launch(sys.argv[1:], args.gpus))
-    loader, wD, wm, wls, sigma_rbf, wsv, wdesc = WORKLOADS[args.workload]
+    loader, wD, wm, wls, sigma_rbf, wsv, wdesc, wn, wr, wew, weu = WORKLOADS[args.workload]
+    for k_, v_ in (("n", wn), ("r", wr), ("epsw", wew), ("epsU", weu)):
+        if getattr(args, k_) is None:
+            setattr(args, k_, v_)
     if args.D is None:
         args.D = wD
     if args.m is None:
@@ -365,9 +396,12 @@ def main():
     C = args.chains
     if C <= 0:
         # filling the GPU: the chain engine whenever it takes the shape (one chain's session
-        # would pick the grid engine, the single-chain latency choice)
+        # would pick the grid engine, the single-chain latency choice); past r = 5 the wave engine
+        # (one chain per CU: 256 chains = 2048 dimension waves, two per SIMD)
         eng = "grid"
-        if args.engine in ("auto", "chain"):
+        if args.engine == "wave" or (args.engine == "auto" and r > 5):
+            eng = "wave"
+        elif args.engine in ("auto", "chain"):
             from gpt_amd._lib import GPTError
             try:
                 probe = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU,
@@ -380,7 +414,8 @@ def main():
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         # chain engine: one chain per CU, two at D <= 4 (4-wave build, 80 KB of LDS);
         # grid engine: D+1 workgroups per chain
-        C = (cus * (2 if D <= 4 else 1)) if eng == "chain" else max(1, cus // (D + 1))
+        C = ((cus * (2 if D <= 4 else 1)) if eng == "chain"
+             else (cus if eng == "wave" else max(1, cus // (D + 1))))
     need = args.warmup + args.steps + args.kernel_steps
     epochs = -(-need // nb) + 1
     epochs_total = max(args.epochs, epochs)
@@ -445,6 +480,19 @@ def main():
     B = m
     bytes_launch = C * algorithmic_bytes_per_step(n, D, B, r, Q)
     achieved = bytes_launch / (k_us * 1e-6) / 1e9
+    if info["engine"] == "wave":
+        # r = 20: fp64-compute bound (§8(d): ≈42.5 MFLOP against 0.9 MB per chain-step)
+        fl = C * algorithmic_flops_per_step(n, D, B, r, Q)
+        tf = fl / (k_us * 1e-6) / 1e12
+        ex = C * executed_flops_per_step(n, D, B, r, Q)
+        roof = {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": tf / FP64_PEAK_TFLOPS, "algorithmic_flops_per_step": fl,
+                "executed_flops_per_step": ex,
+                "executed_frac": ex / (k_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS,
+                "hbm_achieved_GBs": achieved, "hbm_frac": achieved / HBM_PEAK_GBS}
+    else:
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS}
     # HBM traffic per launch is a PMC quantity (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950
     # FETCH doubling): it cannot be read inside this run, so it comes from the stored profile of
     # the same shape, with its tag (scripts/pmc_chain.sh -> profiles/pmc_traffic.json)
@@ -474,6 +522,8 @@ def main():
     fsum_q = torch.zeros(Nte, dtype=torch.float64, device=dev)
     cnt = 0
     fhq = torch.empty((last, Nte), dtype=torch.float64, device=dev)
+    yte_d = torch.from_numpy(np.ascontiguousarray(yte)).to(dev)
+    finals, curve_means = [], []
     for c in range(C):
         if status[c] != 0:
             continue
@@ -481,15 +531,28 @@ def main():
         pred_device(ws, Us, I0, phi_te, n, D, Nte, r, Q, ns, fhq)
         fsum_q += fhq[:ns].sum(dim=0)
         cnt += ns
+        # this chain's per-epoch test-RMSE curve over its last epochs (kin40kExperiment.jl:83)
+        err = fhq[:ns] - yte_d[None, :]
+        curve = (ysd * torch.sqrt((err * err).mean(dim=1))).cpu().numpy()
+        finals.append(float(curve[-1]))
+        curve_means.append(float(curve.mean()))
     torch.cuda.synchronize()
     fmean_q = combine_predictive_mean(fsum_q, cnt)
     rmse_conv = ens_rmse(yte, fmean_q.cpu().numpy(), ysd)
     quality = {"test_rmse": rmse_conv, "epochs": epochs_total, "samples_per_chain": last,
                "chains": C * world, "bailed_out": int(sum(1 for x in status if x != 0)),
                "train_s": quality_train_s,
+               "chain_final_rmse_median": float(np.median(finals)) if finals else None,
+               "chain_curve_mean_median": float(np.median(curve_means)) if curve_means else None,
                "note": "RMSE (original units, ytrainStd x) of the mean prediction over the last %d "
-                       "epoch-end samples of every chain after %d epochs (kin40kExperiment.jl:74-87)"
-                       % (last, epochs_total)}
+                       "epoch-end samples of every chain after %d epochs (kin40kExperiment.jl:74-87); "
+                       "chain_final_rmse_median / chain_curve_mean_median: the median chain's "
+                       "epoch-%d test RMSE and its curve's mean over the last %d epochs (rank 0's "
+                       "chains)" % (last, epochs_total, epochs_total, last)}
+    if args.workload == "kin40k_ref":
+        ref = np.load(os.path.join(ROOT, "tests", "golden", "ref_curves.npz"))["testRMSE_kin40k"]
+        quality["reference"] = {"file": "testRMSE_kin40k.h5 (tests/golden/ref_curves.npz)",
+                                "final": float(ref[-1]), "last50_curve_mean": float(ref[-50:].mean())}
 
     # posterior predictive over every chain's final state as ONE stacked-sample prediction
     # (fp64-MFMA phidotU GEMM with M = S·r, N = Ntest, K = n per dimension, then the V-phase)
@@ -550,7 +613,7 @@ def main():
         out = compose_line(types.SimpleNamespace(
             args=args, value=value, world=world, world_seen=world_seen, warm_ms=warm_ms,
             ms_per_step=ms_per_step, wdesc=wdesc, N=N, Nte=Nte, D=D, n=n, r=r, Q=Q, m=m, C=C,
-            info=info, achieved=achieved, traffic=traffic, traffic_src=traffic_src, k_us=k_us,
+            info=info, roof=roof, traffic=traffic, traffic_src=traffic_src, k_us=k_us,
             k_us_ranks=k_us_ranks, bytes_launch=bytes_launch, steps_run=steps_run, cpu=cpu,
             quality=quality, allreduce_ms=allreduce_ms, npred=npred, pred_ms=pred_ms,
             pred_flop=pred_flop, gemm_ms=gemm_ms, vphase_ms=vphase_ms, rmse_final=rmse_final,

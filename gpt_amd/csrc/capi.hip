@@ -748,6 +748,27 @@ extern "C" int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int6
 
 extern "C" int64_t gpt_sgld_timeline_slots(void) { return kTimeline; }
 
+// Test entry: expm of `count` row-major nn × nn host matrices on the device, by the wave engine's
+// register-blocked Padé (mode 0) or the grid engine's wave_expm (mode 1).
+extern "C" int gpt_debug_expm(int32_t nn, int32_t count, int32_t mode, const double* A, double* E,
+                              int32_t* bad) {
+  if (count < 1 || !A || !E || !bad) { set_error("bad arguments"); return GPT_ERR_BAD_DIMS; }
+  const size_t b = 8 * (size_t)nn * nn * count;
+  DevMem dA, dE, dB;
+  HIPCHK(dA.alloc(b));
+  HIPCHK(dE.alloc(b));
+  HIPCHK(dB.alloc(4 * (size_t)count));
+  HIPCHK(hipMemcpy(dA.p, A, b, hipMemcpyHostToDevice));
+  hipError_t e = launch_expm_check(nn, count, dA.as<double>(), dE.as<double>(), dB.as<int32_t>(),
+                                   mode, nullptr);
+  if (e == hipErrorInvalidValue) { set_error("nn not instantiated"); return GPT_ERR_BAD_DIMS; }
+  HIPCHK(e);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(E, dE.p, b, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(bad, dB.p, 4 * (size_t)count, hipMemcpyDeviceToHost));
+  return GPT_OK;
+}
+
 extern "C" int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, int64_t* out,
                                          double* event_us) {
   if (!s || !out) { set_error("null argument"); return GPT_ERR_BAD_DIMS; }

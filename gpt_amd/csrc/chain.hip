@@ -20,55 +20,14 @@
 
 namespace gpt {
 
-#ifndef CHAIN_EXP_NOSTAGE        // diagnostics only (wrong results): skip the row DMA / V tasks
-#define CHAIN_EXP_NOSTAGE 0
-#endif
-#ifndef CHAIN_EXP_NONOISE        // ablations (wrong results; scripts/ablation_build.sh): U noise
-#define CHAIN_EXP_NONOISE 0       // zeroed, no expm
-#endif
-#ifndef CHAIN_EXP_NOEXPM
-#define CHAIN_EXP_NOEXPM 0
-#endif
-#ifndef CHAIN_EXP_NOV
-#define CHAIN_EXP_NOV 0
-#endif
-#ifndef CHAIN_PRIO                // s_setprio 1 for the second-dispatched half of the waves
-#define CHAIN_PRIO 0
-#endif
-#ifndef CHAIN_SPRIO               // Stiefel-phase priority of waves 4-7: 1 for the noise, 2 whole phase
-#define CHAIN_SPRIO 0
-#endif
-#ifndef CHAIN_TOUCH               // next-batch rows pulled into L2 / Infinity Cache during the
-#define CHAIN_TOUCH 0             // Stiefel phase (rows per dimension; 0 = off)
-#endif
-#ifndef CHAIN_GRAM_MODE           // proj / geod Grams: M and G in one pass (0), M then momᵀmom (2)
-#define CHAIN_GRAM_MODE 2
-#endif
-#ifndef CHAIN_SCTAB               // U-noise angles from an LDS sin/cos table (1) or by polynomial (0)
-#define CHAIN_SCTAB 1
-#endif
-#ifndef CHAIN_OBF                 // (b) butterfly over exactly G·R values (1) or padded to 2^k (0)
-#define CHAIN_OBF 1
-#endif
-#ifndef CHAIN_BFLY
-#define CHAIN_BFLY 1              // (b) reduction: register butterfly (1) or LDS scratch + 8-lane DPP (0)
-#endif
-#ifndef CHAIN_STAGE_AT
-#define CHAIN_STAGE_AT 3          // next group's rows staged at: 0 (a), 1 (c), 2 (e), 3 end of (b), 4 end of (c)
-#endif
-#ifndef CHAIN_DBUF                // two row-staging buffers: group g+1 is staged at the top of
-#define CHAIN_DBUF 0              // iteration g and (e) re-reads its rows from LDS
-#endif
-constexpr int kChainBufs = CHAIN_DBUF ? 2 : 1;
+// Variants measured and dropped in rounds 1-3 (DESIGN.md keeps the numbers) are no longer
+// switchable here: LDS-scratch (b) reductions, padded butterflies, other row-staging points,
+// double-buffered staging, L2 touches of the next batch, wave priorities, the fused M + G Gram.
+constexpr int kChainBufs = 1;     // row-staging buffers
 constexpr int kChainDMax = 8;     // waves per workgroup (one per input dimension)
-#ifndef CHAIN_G
-#define CHAIN_G 2                 // batch rows per group
-#endif
-#ifndef CHAIN_TPW8
-#define CHAIN_TPW8 1              // V tasks per wave at J = 8, D > 4
-#endif
-constexpr int kChainTasks = 2;    // V-phase tasks per wave (NCH·G <= tasks·D); J = 8: CHAIN_TPW8
-constexpr int kChainG = CHAIN_G;  // batch rows per group
+constexpr int kChainTPW8 = 1;     // V tasks per wave at J = 8, D > 4
+constexpr int kChainTasks = 2;    // V-phase tasks per wave (NCH·G <= tasks·D); J = 8: kChainTPW8
+constexpr int kChainG = 2;        // batch rows per group (G = 3 spills 60 VGPRs)
 constexpr int kChainQPL = 4;      // q chunks of 64 (Q <= 64·kChainQPL)
 constexpr int kChainQP = 64 * kChainQPL;
 constexpr int kChainRun = 64;     // members per run (core entries with one value of I[·,k])
@@ -112,7 +71,7 @@ struct ChainLds {
   // after the union: the U noise's (sin, cos)(2πi/256) table (WV = 8 builds; the WV = 4 carve
   // stays under 80 KB for two chains per CU and draws its angles by polynomial)
   static constexpr int o_tab = al16c(o_un + 8 * (L_dbl > x_dbl * WV ? L_dbl : x_dbl * WV));
-  static constexpr bool tab = CHAIN_SCTAB && WV == kChainDMax;
+  static constexpr bool tab = WV == kChainDMax;
   static constexpr int bytes = al16c(o_tab + (tab ? 8 * 512 : 0));
 };
 
@@ -138,14 +97,7 @@ struct ChainLds {
 #ifndef CHAIN_STAMPS
 #define CHAIN_STAMPS CHAIN_SSTAMP
 #endif
-#ifndef CHAIN_SCHED_FENCE
-#define CHAIN_SCHED_FENCE 0
-#endif
-#if CHAIN_SCHED_FENCE
-#define CHAIN_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
 #define CHAIN_FENCE() do {} while (0)
-#endif
 #if !CHAIN_STAMPS
 #define CSTAMP(slot) CHAIN_FENCE()
 #endif
@@ -253,7 +205,6 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   if (t0 >= P.total_steps) return;
   if (__hip_atomic_load(Cp->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   CSTAMP(0);
-  if (CHAIN_PRIO && k >= 4) __builtin_amdgcn_s_setprio(1);
   const long long tend = min(P.total_steps, t0 + (long long)nsteps);
 
   // batch of step tt: its rows of the epoch order and its length
@@ -357,7 +308,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 
 
 
-  constexpr int TPW = (J >= 8 && WV > 4) ? CHAIN_TPW8 : kChainTasks;   // J = 8, D > 4: one task
+  constexpr int TPW = (J >= 8 && WV > 4) ? kChainTPW8 : kChainTasks;   // J = 8, D > 4: one task
   for (;;) {                             // ---------------------------------- one SGLD step
   // thread ids formed inside the step from v_mbcnt (not threadIdx.x): per-lane addresses are not
   // hoisted out of the step loop, and v0 need not be kept — the register-bound kernel used to spill
@@ -410,10 +361,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     // (a) this wave's staged rows -> registers, then stage the next group behind them
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     LSTAMP(1);
-    double* pw = pw0 + (CHAIN_DBUF ? slot * (G * 64 * J) : 0);
-#if CHAIN_DBUF
-    if (g0 + G < Bt) stage(g0 + G, ln, pw0 + (slot ^ 1) * (G * 64 * J));
-#endif
+    double* pw = pw0;
     double p[G][J];
 #pragma unroll
     for (int gg = 0; gg < G; ++gg)
@@ -422,17 +370,13 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         p[gg][jj] = pw[gg * 64 * J + ln + 64 * jj];   // j >= n: finite in-row values, u = 0 there
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     LSTAMP(2);
-#if CHAIN_STAGE_AT == 0 && !CHAIN_DBUF
-    if (g0 + G < Bt) stage(g0 + G, ln, pw);
-#endif
     // (b) temp[k,l,row] and 1/temp for the G rows: R partial dots per lane, reduced through this
     // wave's LDS scratch by 8-lane groups (lane 8l+s sums 8 partials of output l, DPP finishes)
     double* tsl = temp_l + slot * L::TS;
     const int rl = min(ln >> 3, R - 1);
-#if CHAIN_BFLY
     {
       // the G·R partial dots of this lane, reduced over the wave by one register butterfly
-      // (permlane swaps + DPP, no LDS round trip): lane λ ends with the total of value λ >> SH
+      // (permlane swaps + DPP, no LDS round trip) over exactly G·R values (obf_run)
       double v[G * R];
 #pragma unroll
       for (int x = 0; x < G * R; ++x) v[x] = 0.0;
@@ -442,73 +386,26 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
         for (int jj = 0; jj < J; ++jj)
 #pragma unroll
           for (int l = 0; l < R; ++l) v[gg * R + l] = fma(p[gg][jj], u[jj][l], v[gg * R + l]);
-#if CHAIN_OBF
       obf_run<G * R, G * R>(v, ln);
       int vi;
       bool wr;
       obf_index<G * R>(ln, vi, wr);
       if (wr) {
-#else
-      constexpr int NVB = G * R <= 8 ? 8 : (G * R <= 16 ? 16 : (G * R <= 32 ? 32 : 64));
-      constexpr int SH = 6 - Butterfly<NVB>::P;
-      double vb[NVB];
-#pragma unroll
-      for (int x = 0; x < NVB; ++x) vb[x] = x < G * R ? v[x] : 0.0;
-      Butterfly<NVB>::run(vb, ln);
-      v[0] = vb[0];
-      const int vi = ln >> SH;
-      if ((ln & ((1 << SH) - 1)) == 0 && vi < G * R) {
-#endif
         const int gg = vi / R, l = vi - gg * R;
         tsl[(k * R + l) * G + gg] = v[0];
         tsl[DRG + G + (k * R + l) * G + gg] = rcp_nr(v[0]);
       }
     }
-#else
-    const int rs = ln & 7;
-#pragma unroll
-    for (int gg = 0; gg < G; ++gg) {
-      double v[R];
-#pragma unroll
-      for (int l = 0; l < R; ++l) v[l] = 0.0;
-#pragma unroll
-      for (int jj = 0; jj < J; ++jj)
-#pragma unroll
-        for (int l = 0; l < R; ++l) v[l] = fma(p[gg][jj], u[jj][l], v[l]);
-#pragma unroll
-      for (int l = 0; l < R; ++l) bscr[(gg * R + l) * kChainRunS + ln] = v[l];
-    }
-    wave_sync();
-    double sacc[G];
-#pragma unroll
-    for (int gg = 0; gg < G; ++gg) {
-      sacc[gg] = bscr[(gg * R + rl) * kChainRunS + rs];
-#pragma unroll
-      for (int i = 1; i < 8; ++i) sacc[gg] += bscr[(gg * R + rl) * kChainRunS + rs + 8 * i];
-    }
-#pragma unroll
-    for (int gg = 0; gg < G; ++gg) {
-      const double sv = group8_sum(sacc[gg]);
-      if (rs == 0 && (ln >> 3) < R) {
-        tsl[(k * R + rl) * G + gg] = sv;
-        tsl[DRG + G + (k * R + rl) * G + gg] = rcp_nr(sv);
-      }
-    }
-#endif
-#if CHAIN_STAGE_AT == 3 && !CHAIN_DBUF
-    if (!CHAIN_EXP_NOSTAGE && g0 + G < Bt) stage(g0 + G, ln, pw);
-#endif
+    // the next group's rows are staged here, behind (b) (measured best of five placements)
+    if (g0 + G < Bt) stage(g0 + G, ln, pw);
     LSTAMP(3);
     lds_barrier();
     LSTAMP(4);
-#if CHAIN_STAGE_AT == 1 && !CHAIN_DBUF
-    if (g0 + G < Bt) stage(g0 + G, ln, pw);
-#endif
     // (c) V tasks: task = gg·NCH + c covers q = 64c + lane of batch column g0+gg
 #pragma unroll
     for (int x = 0; x < TPW; ++x) {
       const int task = k + D * x;
-      if (task >= NT || CHAIN_EXP_NOV) break;
+      if (task >= NT) break;
       const int gg = task / NCH, c = task - gg * NCH;
       const int q = 64 * c + ln;
       const bool ok = q < Q;
@@ -527,15 +424,9 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       const double fs = wave_sum(wV);
       if (lane == 0) fp_l[gg * kChainQPL + c] = fs;
     }
-#if CHAIN_STAGE_AT == 4 && !CHAIN_DBUF
-    if (g0 + G < Bt) stage(g0 + G, ln, pw);
-#endif
     LSTAMP(5);
     lds_barrier();
     LSTAMP(6);
-#if CHAIN_STAGE_AT == 2 && !CHAIN_DBUF
-    if (!CHAIN_EXP_NOSTAGE && g0 + G < Bt) stage(g0 + G, ln, pw);
-#endif
     // (e) residuals, A[:,k,·]·res, and the gradU / gradw accumulation
     double res[G];
 #pragma unroll
@@ -561,11 +452,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       for (int l = 0; l < R; ++l) cc[l] = readlane_d(a, 8 * l);
 #pragma unroll
       for (int jj = 0; jj < J; ++jj) {
-#if CHAIN_DBUF
-        const double pv = pw[gg * 64 * J + ln + 64 * jj];
-#else
         const double pv = p[gg][jj];
-#endif
 #pragma unroll
         for (int l = 0; l < R; ++l) acc[jj][l] = fma(pv, cc[l], acc[jj][l]);
       }
@@ -643,26 +530,11 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) rows0[gg] = gptr(ordn)[min(gg, Bn - 1)];
     stage_rows(rows0, lane, pw0);
-    if constexpr (CHAIN_TOUCH > 0) {
-      // one 4-B piece per 128-B line of the next batch's first rows (lanes 0..31 span a 4-KB
-      // row slice): the lines land in L2 / the Infinity Cache while HBM is otherwise idle; the
-      // bytes go to a sink in LDS that nothing reads
-      __attribute__((address_space(3))) void* sink =
-          (__attribute__((address_space(3))) void*)(smem + L::o_touch);
-      const unsigned o = min(128u * (unsigned)(lane & 31), 8u * n - 4u);
-      for (int i = 0; i < CHAIN_TOUCH; ++i) {
-        const int row = gptr(ordn)[min(G + i, Bn - 1)];
-        const char* rb = (const char*)(phi_k + (long long)row * rstride);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(rb + o),
-                                         sink, 4, 0, 0);
-      }
-    }
   }
   CSTAMP(3);
   SSTAMP(3);
 
   // ---- U^(k): gradient, Langevin drive, Stiefel projection + geodesic (per wave)
-  if (CHAIN_SPRIO && k >= 4) __builtin_amdgcn_s_setprio(1);
   const double cU = cN / C.signal_var;
   const double sq = sqrt(C.epsU);
   double gu2 = 0.0;
@@ -679,16 +551,12 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
 #pragma unroll
       for (int q = 0; q < NQJ; ++q) {
         double z[4];
-        if (CHAIN_EXP_NONOISE) {
-          z[0] = z[1] = z[2] = z[3] = 0.0;
-        } else {
-          if constexpr (L::tab)
-            normal_quad_tab<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
-                                (uint32_t)k, (const double*)(smem + L::o_tab), z);
-          else
-            normal_quad<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
-                            (uint32_t)k, z);
-        }
+        if constexpr (L::tab)
+          normal_quad_tab<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
+                              (uint32_t)k, (const double*)(smem + L::o_tab), z);
+        else
+          normal_quad<NZ>(C.seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
+                          (uint32_t)k, z);
 #pragma unroll
         for (int i = 0; i < NZ; ++i)
           if (4 * q + i < J) xi_l[(4 * q + i) * 64 + lane] = z[i];
@@ -711,7 +579,6 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     gu2 = wave_sum(gu2);
     if (lane == 0) C.diag[(size_t)t * (1 + D) + 1 + k] = sqrt(gu2);
   }
-  if (CHAIN_SPRIO == 1) __builtin_amdgcn_s_setprio(0);
   CSTAMP(4);
   SSTAMP(4);
   {
@@ -728,24 +595,19 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     // needs A = Uᵀmom and S = momᵀmom.  With UᵀU = I, A = (M − Mᵀ)/2 and
     // S = G − MᵀMs − Ms·M + Ms·Ms for the drive's Gram G = WᵀW (the oracle's reference form
     // agrees to ≤ 1.2e-14 relative over whole trajectories, tests/test_oracle.py), so Uᵀmom
-    // needs no pass over the rows.  CHAIN_GRAM_MODE 0: M and G from one pass (row a reduces
-    // M[a,:] and G[a,a:] in one butterfly); 2: M, then S = momᵀmom from a second pass after mom.
+    // needs no pass over the rows.  M, then S = momᵀmom from a second pass after mom (M and G
+    // from one pass spilled u into the batch loop, round 3).
 #pragma unroll
     for (int a = 0; a < R; ++a) {
-      double v[2 * R];
+      double v[R];
 #pragma unroll
       for (int bb = 0; bb < R; ++bb) {
-        double s0 = 0.0, s1 = 0.0;
+        double s0 = 0.0;
 #pragma unroll
-        for (int jj = 0; jj < J; ++jj) {
-          s0 = fma(u[jj][a], acc[jj][bb], s0);
-          if (CHAIN_GRAM_MODE == 0 && bb >= a) s1 = fma(acc[jj][a], acc[jj][bb], s1);
-        }
+        for (int jj = 0; jj < J; ++jj) s0 = fma(u[jj][a], acc[jj][bb], s0);
         v[bb] = s0;
-        v[R + bb] = s1;
       }
-      if constexpr (CHAIN_GRAM_MODE == 0) wave_sum_to_lds<R>(v, Mg + a * R, Sg + a * R);
-      else wave_sum_to_lds<R>(*(double(*)[R])v, Mg + a * R);
+      wave_sum_to_lds<R>(v, Mg + a * R);
     }
     wave_sync();
     SSTAMP(5);
@@ -764,7 +626,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     }
       CSTAMP(5);
       SSTAMP(6);
-      if constexpr (CHAIN_GRAM_MODE == 2) {
+      {
 #pragma unroll
         for (int a = 0; a < R; ++a) {
           double v[R];
@@ -784,23 +646,6 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
           Ag[o] = (Mg[o] - Mg[b * R + i]) / 2;
           if (i > b) Sg[o] = Sg[b * R + i];
         }
-      } else {
-        // lanes < r² form A[i][b] and S[i][b] (a short loop: U and the drive stay in registers)
-        if (lane < R * R) {
-          const int i = lane / R, b = lane - i * R;
-          double s = Sg[min(i, b) * R + max(i, b)];
-#pragma unroll 1
-          for (int c = 0; c < R; ++c) {
-            const double mci = Mg[c * R + i], mic = Mg[i * R + c];
-            const double mcb = Mg[c * R + b], mbc = Mg[b * R + c];
-            const double msic = (mic + mci) / 2, mscb = (mcb + mbc) / 2;
-            s = fma(-mci, mscb, s);
-            s = fma(-msic, mcb, s);
-            s = fma(msic, mscb, s);
-          }
-          Ag[lane] = (Mg[lane] - Mg[b * R + i]) / 2;
-          Sg[lane] = s;                       // after this wave's G reads (in-order LDS)
-        }
       }
       wave_sync();
       const double tt = sq;
@@ -814,13 +659,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       wave_sync();
       long long* xst = (CHAIN_SSTAMP && P.stamps && k == 0)
                            ? P.stamps + (size_t)(4 * gridDim.x + blockIdx.x) * kStamps : nullptr;
-      bool bad = false;
-      if (CHAIN_EXP_NOEXPM) {                 // ablation: E = the input (no Padé)
-        for (int o = lane; o < NN * NN; o += 64) X0[NN * NN + o] = X0[o];
-        wave_sync();
-      } else {
-        bad = wave_expm<NN>(X0, xst);
-      }
+      const bool bad = wave_expm<NN>(X0, xst);
       SSTAMP(7);
       for (int o = lane; o < NN * R; o += 64) {
         const int a = o / R, l = o - a * R;
@@ -830,12 +669,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       double* X1 = X0;                        // expm(−tA) in the same scratch
       for (int o = lane; o < R * R; o += 64) X1[o] = -tt * Ag[o];
       wave_sync();
-      if (CHAIN_EXP_NOEXPM) {
-        for (int o = lane; o < R * R; o += 64) X1[R * R + o] = X1[o];
-        wave_sync();
-      } else {
-        wave_expm<R>(X1, xst ? xst + (size_t)gridDim.x * kStamps : nullptr);
-      }
+      wave_expm<R>(X1, xst ? xst + (size_t)gridDim.x * kStamps : nullptr);
       if (bad && lane == 0) flag[0] = 1;
       CSTAMP(6);
       SSTAMP(8);
@@ -904,7 +738,6 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
     SSTAMP(13);
     if (CHAIN_STAMPS && P.stamps && lane == 0)   // per-wave arrival at the end-of-step barrier
     P.stamps[(size_t)blockIdx.x * kStamps + 8 + k] = (long long)__builtin_amdgcn_s_memtime();
-  if (CHAIN_SPRIO == 2) __builtin_amdgcn_s_setprio(0);
   __syncthreads();                      // w_l, flag and the gradw partials are complete
     if (C.diag && tid == 0) {
       double s = 0.0;
@@ -970,7 +803,7 @@ bool chain_supported(int n, int D, int r, int Q, int m, bool langevin, bool stie
   if (chain_J(n) >= 2 && (n & 1)) return false;   // 16-B row staging needs 16-B aligned rows
   if (Q > kChainQP || m > kChainMMax) return false;   // the fixed LDS carve's maxima
   const int NT = (Q + 63) / 64 * kChainG;
-  if (NT > ((chain_J(n) >= 8 && D > 4) ? CHAIN_TPW8 : kChainTasks) * D) return false;
+  if (NT > ((chain_J(n) >= 8 && D > 4) ? kChainTPW8 : kChainTasks) * D) return false;
   return chain_lds_bytes(n, D, r, Q, m) + chain_static_lds(chain_J(n), chain_wv(D)) <= 160 * 1024;
 }
 

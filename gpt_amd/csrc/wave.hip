@@ -92,7 +92,8 @@ __device__ __forceinline__ double blk_id(int lane, int x, int y) {
 // degree 13 with 2^-s scaling above), with the polynomial terms in registers.  Returns true if
 // the result holds a NaN (the geod bail-out, GPT_SGLD.jl:23-26).
 template <int NN>
-__device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int lane) {
+__device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int lane,
+                                        long long* st = nullptr) {
   constexpr int BS = Blk<NN>::BS;
   double cs = 0.0;
   if (lane < NN) {
@@ -199,6 +200,7 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
       }
   }
   wave_sync();                                           // every operand read is done
+  if (st && lane == 0) st[0] = (long long)__builtin_amdgcn_s_memtime();
   {
     Blk<NN> M;
 #pragma unroll
@@ -216,6 +218,7 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
   if constexpr (2 * NN <= 64) solved = wave_solve_dd<NN>(S0, S1);
   else if constexpr (NN <= 64) solved = wave_solve_dd2<NN>(S0, S1, S2);
   if (!solved) wave_solve<NN>(S0, S1);
+  if (st && lane == 0) st[1] = (long long)__builtin_amdgcn_s_memtime();
   for (int z = 0; z < si; ++z) {
     Blk<NN> P2;
     blk_mm<NN>(S1, S1, P2, lane);
@@ -283,8 +286,8 @@ GPT_HD int wv_dim_lds_dbl(int n, int r, int m) {
 // The V-phase workgroup's LDS (doubles): temp of the batch, V (stride m|1), w, y, res, fhat
 // partials and a reduction row.
 GPT_HD int wv_vphase_lds_dbl(int D, int r, int Q, int m) {
-  const int ints = Q * D + D * Q + D * (r + 1);          // temp offsets, run members, run starts
-  return D * r * m + (Q + 1) * (m | 1) + Q + 1 + 2 * 64 + 8 * 64 + 8 + (ints + 1) / 2;
+  const int shorts = Q * D + D * Q + D * (r + 1);        // temp offsets, run members, run starts
+  return D * r * m + (Q + 1) * (m | 1) + Q + 1 + 2 * 64 + 8 * 64 + 8 + (shorts + 3) / 4;
 }
 
 constexpr int kWvMaxM = 64;            // minibatch rows: one per lane of the V-phase
@@ -319,9 +322,11 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
   double* res_l = y_l + 64;
   double* fpart = res_l + 64;                         // [wave·64 + i]
   double* red = fpart + 8 * 64;
-  int* toff_l = (int*)(red + 8);                      // [q·D + k] = (k·R + I[q,k])·m
-  int* mem_l = toff_l + Q * D;                        // run members (wave_tables), then starts
-  int* seg_l = mem_l + D * Q;
+  // 16-bit tables: [q·D + k] = (k·R + I[q,k])·m (< 2^16, wave_supported), the run members
+  // (wave_tables), then the run starts
+  unsigned short* toff_l = (unsigned short*)(red + 8);
+  unsigned short* mem_l = toff_l + Q * D;
+  unsigned short* seg_l = mem_l + D * Q;
 
   const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
   const int Bt = min(m, P.N - b * m);
@@ -336,9 +341,9 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
     if (tid < 64) y_l[tid] = tid < Bt ? gptr(Cp->y)[gptr(ord)[tid]] : 0.0;
     for (int o = tid; o < Q * D; o += 512) {
       const int q = o / D, k = o - q * D;
-      toff_l[o] = (k * R + gptr(P.I0)[q + Q * k]) * m;
+      toff_l[o] = (unsigned short)((k * R + gptr(P.I0)[q + Q * k]) * m);
     }
-    copy_to_lds<4>(mem_l, P.wvtab, D * Q + D * (R + 1), tid, 512);
+    for (int o = tid; o < D * Q + D * (R + 1); o += 512) mem_l[o] = (unsigned short)gptr(P.wvtab)[o];
   }
   __syncthreads();
   // V[q,i] = Π_k temp[k, I[q,k], i] in k order (computeV) and w_q·V partial sums of fhat:
@@ -348,7 +353,7 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
     const int Qw = (Q + 7) / 8, qa = wv * Qw, qb = min(Q, qa + Qw);
     double f = 0.0;
     for (int q = qa; q < qb; ++q) {
-      const int* to = toff_l + q * D;
+      const unsigned short* to = toff_l + q * D;
       double v = temp_l[to[0] + ic];
       for (int k = 1; k < D; ++k) v *= temp_l[to[k] + ic];
       if (i < Bt) V_l[q * MV + i] = v;
@@ -399,7 +404,7 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
     for (int p = wv; p < D * R; p += 8) {
       const int k = p / R, l = p - k * R;
       const int s0 = seg_l[k * (R + 1) + l], s1 = seg_l[k * (R + 1) + l + 1];
-      const int* mk = mem_l + k * Q;
+      const unsigned short* mk = mem_l + k * Q;
       double a = 0.0;
       for (int s = s0; s < s1; s += 4) {               // members 4 at a time (past the run: q = Q,
         int q4[4];                                      // a zero row and a zero weight)
@@ -683,7 +688,7 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
     for (int o = lane; o < R * R; o += 64) X1[o] = -tt * Ag[o];
     wave_sync();
     WSTAMP(srow, 6);
-    wv_expm<R>(X1, X1b, X1c, lane);
+    wv_expm<R>(X1, X1b, X1c, lane, P.stamps ? P.stamps + (size_t)srow * kStamps + 14 : nullptr);
     WSTAMP(srow, 7);
 #pragma unroll
     for (int x = 0; x < MXL; ++x) mxr[x] = X1b[min(lane + 64 * x, R * R - 1)];
@@ -697,7 +702,7 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
       S0[o] = tt * v;
     }
     wave_sync();
-    bad = wv_expm<NN>(S0, S1, S2, lane);
+    bad = wv_expm<NN>(S0, S1, S2, lane, P.stamps ? P.stamps + (size_t)srow * kStamps + 12 : nullptr);
   }
   WSTAMP(srow, 8);
   // F = E[:, 1:r]·expm(−tA) (2r × r) into slot 0; expm(−tA) back to LDS at slot 2
@@ -804,6 +809,7 @@ bool wave_supported(int n, int D, int r, int Q, int m, bool langevin, bool stief
 #undef CASE
   if (!inst || wv_J(n) == 0 || m > kWvMaxM || D < 1 || D > kDMax) return false;
   if (3 * r * r > n * r) return false;            // expm(−tA)'s scratch below the Grams
+  if ((long long)D * r * m >= 65536 || Q >= 65536) return false;   // 16-bit V-phase tables
   return wv_vphase_lds_bytes(D, r, Q, m) <= 160 * 1024 && wv_dim_lds_bytes(n, r, m) <= 160 * 1024;
 }
 
@@ -857,4 +863,49 @@ hipError_t launch_wave(const StepParams& P, const ChainDesc* chains, int nchains
   return hipErrorInvalidValue;
 }
 
+}  // namespace gpt
+
+// ------------------------------------------------------------------------ expm unit check (tests)
+namespace gpt {
+// One wave per matrix: wv_expm (mode 0) or the grid engine's wave_expm (mode 1) of an NN × NN
+// row-major matrix; NaN flags in bad.
+template <int NN>
+__global__ __launch_bounds__(64) void wv_expm_check_kernel(const double* A, double* E, int32_t* bad,
+                                                           int mode) {
+  extern __shared__ __attribute__((aligned(16))) double wv_sm[];
+  const int lane = lane_id();
+  const double* a = A + (size_t)blockIdx.x * NN * NN;
+  double* S0 = wv_sm;
+  for (int o = lane; o < NN * NN; o += 64) S0[o] = a[o];
+  wave_sync();
+  bool b;
+  const double* res;
+  if (mode == 0) {
+    b = wv_expm<NN>(S0, S0 + NN * NN, S0 + 2 * NN * NN, lane);
+    res = S0 + NN * NN;
+  } else {
+    b = wave_expm<NN>(S0);
+    res = S0 + NN * NN;
+  }
+  wave_sync();
+  for (int o = lane; o < NN * NN; o += 64) E[(size_t)blockIdx.x * NN * NN + o] = res[o];
+  if (lane == 0) bad[blockIdx.x] = b ? 1 : 0;
+}
+
+hipError_t launch_expm_check(int nn, int count, const double* A, double* E, int32_t* bad, int mode,
+                             hipStream_t st) {
+#define CASE(NNV)                                                                               \
+  if (nn == NNV) {                                                                              \
+    const size_t lds = 8 * (size_t)7 * NNV * NNV;                                               \
+    hipError_t e = hipFuncSetAttribute((const void*)wv_expm_check_kernel<NNV>,                 \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+    if (e != hipSuccess) return e;                                                              \
+    hipLaunchKernelGGL(wv_expm_check_kernel<NNV>, dim3(count), dim3(64), lds, st, A, E, bad,    \
+                       mode);                                                                   \
+    return hipGetLastError();                                                                   \
+  }
+  CASE(12) CASE(16) CASE(20) CASE(24) CASE(30) CASE(32) CASE(40)
+#undef CASE
+  return hipErrorInvalidValue;
+}
 }  // namespace gpt

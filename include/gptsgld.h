@@ -159,6 +159,11 @@ int gpt_sgld_session_stamps(gpt_sgld_session* s, int64_t nsteps, int64_t* out);
  * library fills slots 0, 1 and the last step's; the timeline build (`make timeline`) every step.
  * *event_us = the launch's hipEvent time. */
 int64_t gpt_sgld_timeline_slots(void);
+/* Test entry: E = expm(A) for `count` row-major nn x nn host matrices (nn in {12,16,20,24,30,32,
+ * 40}) on the device: mode 0 the wave engine's register-blocked Padé (wave.hip wv_expm), mode 1 the
+ * grid engine's wave_expm; bad[c] = 1 when E_c holds a NaN (the geodesic bail-out test). */
+int gpt_debug_expm(int32_t nn, int32_t count, int32_t mode, const double* A, double* E,
+                   int32_t* bad);
 int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, int64_t* out, double* event_us);
 /* Copy chain c's stores / status back (status: GPT_OK or GPT_ERR_NAN_GEODESIC; stores are
  * zero-filled for a non-zero status). */

