@@ -119,7 +119,7 @@ def test_bench_line_fields_at_world_2():
     common = dict(args=args, value=5.0e6, warm_ms=300.0, ms_per_step=0.1, wdesc="kin40k", N=10000,
                   Nte=30000, D=8, n=500, r=5, Q=200, m=50, C=256,
                   info=dict(engine="chain", workgroups=256, threads=512, lds_bytes=73600),
-                  achieved=5000.0, traffic=4.2e8, traffic_src="t", bytes_launch=4.94e8,
+                  roof={"bound": "hbm", "achieved": 5000.0, "peak": 8000.0, "unit": "GB/s", "frac": 0.625}, traffic=4.2e8, traffic_src="t", bytes_launch=4.94e8,
                   steps_run=41000, cpu=dict(value=17000.0, cores=16, kind="port"),
                   quality=quality, allreduce_ms=0.05, npred=256, pred_ms=6.9, pred_flop=3.07e11,
                   gemm_ms=5.4, vphase_ms=1.0, rmse_final=0.28,
