@@ -513,9 +513,27 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   return GPT_OK;
 }
 
-// Overwrite chain c's initial state (w_init/U_init injection of the host API).
+// Overwrite chain c's initial state (w_init/U_init injection of the host API).  On the Stiefel
+// path the kernels take geod's A = Uᵀmom as (M − Mᵀ)/2 (and the grid engine S from the Gram
+// identity), which holds only for UᵀU = I: a U_init off the manifold is rejected.
 static int session_set_state(gpt_sgld_session* s, int c, const double* w, const double* U) {
   const ChainDesc& C = s->chains_h[c];
+  if (U && s->cfg.stiefel) {
+    const int n = s->P.n, r = s->P.r, D = s->P.D;
+    for (int k = 0; k < D; ++k) {
+      const double* Uk = U + (size_t)n * r * k;
+      for (int a = 0; a < r; ++a)
+        for (int b = a; b < r; ++b) {
+          double g = 0.0;
+          for (int j = 0; j < n; ++j) g += Uk[j + (size_t)n * a] * Uk[j + (size_t)n * b];
+          if (std::fabs(g - (a == b ? 1.0 : 0.0)) > 1e-10) {
+            set_error("U_init must have orthonormal columns in every dimension (max |U_kᵀU_k - I| "
+                      "<= 1e-10) on the Stiefel path");
+            return GPT_ERR_BAD_DIMS;
+          }
+        }
+    }
+  }
   if (w) HIPCHK(hipMemcpy(C.w, w, 8 * (size_t)s->P.Q, hipMemcpyHostToDevice));
   if (U) HIPCHK(hipMemcpy(C.U, U, 8 * (size_t)s->P.n * s->P.r * s->P.D, hipMemcpyHostToDevice));
   s->temp_ready = false;
@@ -1200,6 +1218,11 @@ extern "C" int gpt_pred_dev(const double* w_dev, const double* U_dev, const int3
   hipError_t e = launch_pred(w_dev, U_dev, I0_dev, phitest_dev, (int)n, (int)D, Ntest, (int)r,
                              (int)Q, (int)S, fhat_dev, (hipStream_t)hip_stream);
   if (e != hipSuccess) return hip_fail(e, "pred kernel");
+  return GPT_OK;
+}
+
+extern "C" int gpt_pred_trim_pool(void) {
+  HIPCHK(pred_trim_pools());
   return GPT_OK;
 }
 

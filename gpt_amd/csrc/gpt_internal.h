@@ -217,6 +217,7 @@ struct PredPhaseTiming { double gemm_ms = 0.0, vphase_ms = 0.0; };
 hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, const double* phitest,
                        int n, int D, long long Ntest, int r, int Q, int S, double* fhat,
                        hipStream_t st, PredPhaseTiming* timing = nullptr);
+hipError_t pred_trim_pools();      // return the prediction pool's memory (gpt_pred_trim_pool)
 hipError_t launch_mean_rmse(const double* fhat, const double* ytest, long long Ntest, int S,
                             double* mean_out, double* sse_out, hipStream_t st);
 hipError_t launch_feature(const double* X, long long N, int D, const double* ls, double c,

@@ -1,5 +1,7 @@
 // Test-set prediction and RMSE reductions (GPT_SGLD.jl:233-243; GPT_SGLD_p.jl:124-132;
 // kin40kExperiment.jl:78-87).
+#include <mutex>
+
 #include "device_util.h"
 
 #include <algorithm>
@@ -558,6 +560,44 @@ static hipError_t vphase_pairs(int NTp, const double* w, const double* T, const 
   }
 }
 
+// The prediction's pass buffers come from a private stream-ordered pool per device that keeps its
+// memory between calls (release threshold ∞: the default threshold 0 unmapped and remapped the
+// ~GBs of every call, ≈0.45 ms of a 7 ms call) without changing the device's default pool for the
+// rest of the process; gpt_pred_trim_pool() returns it.
+static std::mutex g_pred_pool_mu;
+static hipMemPool_t g_pred_pool[64] = {};
+
+static hipError_t pred_pool(hipMemPool_t* out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(g_pred_pool_mu);
+  hipMemPool_t& p = g_pred_pool[dev & 63];
+  if (!p) {
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    e = hipMemPoolCreate(&p, &props);
+    if (e != hipSuccess) { p = nullptr; return e; }
+    uint64_t thr = ~0ull;
+    e = hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &thr);
+    if (e != hipSuccess) return e;
+  }
+  *out = p;
+  return hipSuccess;
+}
+
+hipError_t pred_trim_pools() {
+  std::lock_guard<std::mutex> lk(g_pred_pool_mu);
+  for (auto& p : g_pred_pool)
+    if (p) {
+      const hipError_t e = hipMemPoolTrimTo(p, 0);
+      if (e != hipSuccess) return e;
+    }
+  return hipSuccess;
+}
+
 static hipError_t launch_pred_mfma(const double* w, const double* U, const int32_t* I0,
                                    const double* phitest, int n, int D, long long Ntest, int r,
                                    int Q, int S, double* fhat, hipStream_t st,
@@ -576,30 +616,27 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
   // 128 / gcd(128, r) samples, so its S·r columns fill whole 128-column tiles (no MFMA padding)
   const size_t per_sample = 8 * (size_t)D * r * (size_t)Ntest;
   int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)S, ((size_t)8 << 30) / per_sample));
-  // the pass buffer comes from the device's default stream-ordered pool; keep what the pool holds
-  // between calls (a release threshold of 0 would unmap and remap the ~GBs of every call)
-  {
-    static std::atomic<uint64_t> kept{0};
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess && !(kept.load() & (1ull << (dev & 63)))) {
-      hipMemPool_t pool;
-      if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t thr = ~0ull;
-        if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr) == hipSuccess)
-          kept.fetch_or(1ull << (dev & 63));
-      }
-    }
-  }
+  int unit = 1;
   {
     int g = 128, b = r;
     while (b) { const int t = g % b; g = b; b = t; }
-    const int unit = 128 / g;
+    unit = 128 / g;
     if (chunk < S && chunk >= unit) chunk = chunk / unit * unit;
   }
+  hipMemPool_t pool = nullptr;
+  hipError_t e = pred_pool(&pool);
+  if (e != hipSuccess) return e;
   double* T = nullptr;
-  const size_t tbytes = (per_sample * chunk + 255) / 256 * 256;
   const int NTp = pred_pair_tables(D);
-  hipError_t e = hipMallocAsync((void**)&T, tbytes + 4 * (size_t)Q * D + 4 * (size_t)Q * NTp, st);
+  size_t tbytes = 0;
+  for (;;) {          // out of device memory: halve the pass (whole 128-column tiles while it can)
+    tbytes = (per_sample * chunk + 255) / 256 * 256;
+    e = hipMallocFromPoolAsync((void**)&T, tbytes + 4 * (size_t)Q * D + 4 * (size_t)Q * NTp, pool,
+                               st);
+    if (e != hipErrorOutOfMemory || chunk == 1) break;
+    (void)hipGetLastError();
+    chunk = chunk / 2 >= unit ? chunk / 2 / unit * unit : std::max(1, chunk / 2);
+  }
   if (e != hipSuccess) return e;
   int32_t* offs = (int32_t*)((char*)T + tbytes);
   int32_t* offp = offs + (size_t)Q * D;

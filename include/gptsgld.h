@@ -192,6 +192,9 @@ int gpt_pred(const double* w, const double* U, const int32_t* I, const double* p
 int gpt_pred_dev(const double* w_dev, const double* U_dev, const int32_t* I0_dev,
                  const double* phitest_dev, int64_t n, int64_t D, int64_t Ntest, int64_t r,
                  int64_t Q, int64_t S, double* fhat_dev, void* hip_stream);
+/* The stacked-sample prediction keeps its pass buffers (up to 8 GiB) in a private stream-ordered
+ * pool between calls; this returns that memory to the device. */
+int gpt_pred_trim_pool(void);
 /* gpt_pred_dev with per-phase event timing (diagnostics / the benchmark): ms_out[0] = the
  * phidotU GEMM (fp64 MFMA) kernels, ms_out[1] = the V-phase kernels, summed over the sample
  * chunks of the call; synchronises hip_stream. */

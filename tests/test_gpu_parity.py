@@ -614,3 +614,18 @@ def test_device_expm_all_pade_degrees(nn, mode):
     assert not bad.any()
     for c in range(len(mats)):
         assert rel(E[c], want[c]) < 1e-12, (c, rel(E[c], want[c]))
+
+
+def test_injected_U_off_the_manifold_is_rejected():
+    """On the Stiefel path the kernels take geod's A = Uᵀmom from the projection's Gram (valid for
+    UᵀU = I only): a U_init with non-orthonormal columns is refused (GPT_ERR_BAD_DIMS)."""
+    from gpt_amd._lib import GPTError
+    n, D, N, r, Q, m = 12, 3, 30, 2, 6, 10
+    p = make_problem(n, D, N, r, Q, seed=8)
+    _, U0 = R.init_state(n, r, D, Q, 999)
+    with pytest.raises(GPTError):
+        G().GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e-6, 0, 1, 4,
+                          U_init=1.01 * U0)
+    # Euclidean runs take any U
+    G().GPTregression(p["phi"], p["y"], 0.1, p["I"], r, Q, m, 1e-4, 1e-6, 0, 1, 4,
+                      U_init=1.01 * U0, stiefel=False)
