@@ -434,11 +434,11 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
   }
   P.wvtab = nullptr;
   if (s->engine == kEngineWave) {
-    std::vector<int32_t> wt;
-    wave_tables(I0, Q, D, r, wt);
-    HIPCHK(s->wvtab.alloc(sizeof(int32_t) * wt.size()));
-    HIPCHK(hipMemcpy(s->wvtab.p, wt.data(), sizeof(int32_t) * wt.size(), hipMemcpyHostToDevice));
-    P.wvtab = s->wvtab.as<int32_t>();
+    std::vector<uint16_t> wt;
+    wave_tables(I0, Q, D, r, m, wt);
+    HIPCHK(s->wvtab.alloc(sizeof(uint16_t) * wt.size()));
+    HIPCHK(hipMemcpy(s->wvtab.p, wt.data(), sizeof(uint16_t) * wt.size(), hipMemcpyHostToDevice));
+    P.wvtab = s->wvtab.as<uint16_t>();
   }
   P.vtab = nullptr;
   if (s->engine != kEngineChain && s->engine != kEngineWave && step_layout(n, D, r, Q, m).vcols) {

@@ -58,8 +58,8 @@ struct StepParams {
   const int32_t* vtab;            // grid engine, column-lane V-phase: per workgroup kind (k < D,
                                   // w block = D) and core entry q, 16 ints: 8 temp row offsets
                                   // and I[q, k] (vphase_cols_tables), or null (vphase_tile)
-  const int32_t* wvtab;           // wave engine: D*Q run members (q with I[q,k] = l, q order, runs
-                                  // in l order) then D*(r+1) run starts (wave_tables)
+  const uint16_t* wvtab;          // wave engine: V-phase temp offsets, run members, run starts
+                                  // (16-bit, wave_tables)
   long long* stamps;              // diagnostic builds: s_memtime per phase per block, else null
   long long* tline;               // chain engine: per-workgroup timeline (kTimeline per block) or null
   int rms;                        // 1: GPT_SGLDERM_RMSprop steps (grid engine, two launches)
@@ -198,7 +198,8 @@ hipError_t launch_chain(const StepParams& P, const ChainDesc* chains, int nchain
 // Wave engine (wave.hip): two launches per step (V-phase per chain, then a wave per dimension);
 // init = the first step's temp only.
 bool wave_supported(int n, int D, int r, int Q, int m, bool langevin, bool stiefel);
-void wave_tables(const std::vector<int32_t>& I0, int Q, int D, int r, std::vector<int32_t>& out);
+void wave_tables(const std::vector<int32_t>& I0, int Q, int D, int r, int m,
+                 std::vector<uint16_t>& out);
 size_t wv_dim_lds_bytes(int n, int r, int m);
 size_t wv_vphase_lds_bytes(int D, int r, int Q, int m);
 hipError_t launch_wave(const StepParams& P, const ChainDesc* chains, int nchains,

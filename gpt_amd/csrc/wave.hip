@@ -87,6 +87,72 @@ __device__ __forceinline__ double blk_id(int lane, int x, int y) {
   return i0 + x == j0 + y ? 1.0 : 0.0;
 }
 
+// Solve M·X = X0 (X holds X0) for column diagonally dominant M with 32 < NN <= 64: wave_solve_dd's
+// one-pass register LU (Gaussian elimination that partial pivoting provably leaves unswapped;
+// multipliers and pivot rows broadcast by v_readlane, no LDS round trip between pivots) in
+// ⌈NN / (64 − NN)⌉ passes, each over [M | the next 64 − NN columns of X] with one column per
+// lane.  M is re-factored in every pass with the same operations, so every column sees exactly
+// the doubles of wave_solve_dd.  (The two-pass wave_solve_dd2 parks the factors in LDS and
+// writes a pivot's multipliers from one lane: 75 k cycles at NN = 40; two columns per lane in
+// one pass spilled ~1 400 VGPRs.)  Returns false (nothing written) when M is not diagonally
+// dominant.
+template <int NN>
+__device__ __forceinline__ void wv_solve_dd_pass(const double* M, double* X, int xo, int lane) {
+  constexpr int NX = 64 - NN;                            // right-hand sides per pass
+  const bool xl = lane >= NN;
+  const int xc = min(xo + lane - NN, NN - 1);            // this lane's X column (clamped)
+  const bool xw = xl && xo + lane - NN < NN;             // ... and whether it is written
+  double col[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) col[i] = xl ? X[i * NN + xc] : M[i * NN + min(lane, NN - 1)];
+  double rpv[NN];
+#pragma unroll
+  for (int p = 0; p < NN; ++p) {                        // forward elimination (getrf + L solve)
+    const double rp = rcp_nr(readlane_d(col[p], p));
+    rpv[p] = rp;
+#pragma unroll
+    for (int i = p + 1; i < NN; ++i) {
+      const double f = readlane_d(col[i], p) * rp;
+      col[i] -= f * col[p];
+    }
+  }
+#pragma unroll
+  for (int k = NN - 1; k >= 0; --k) {                   // back substitution, column-oriented
+    double u[NN];
+#pragma unroll
+    for (int i = 0; i < k; ++i) u[i] = readlane_d(col[i], k);    // U[0..k-1][k] from lane k
+    if (xl) {
+      col[k] = col[k] * rpv[k];
+#pragma unroll
+      for (int i = 0; i < k; ++i) col[i] -= col[k] * u[i];
+    }
+  }
+  wave_sync();                                           // every lane has read its X column
+  if (xw) {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) X[i * NN + xc] = col[i];
+  }
+  wave_sync();
+  (void)NX;
+}
+
+template <int NN>
+__device__ __forceinline__ bool wv_solve_dd_passes(const double* M, double* X, int lane) {
+  static_assert(NN > 32 && NN < 64, "one X column per lane beside M's");
+  bool dd = true;
+  if (lane < NN) {
+    double off = 0.0;
+#pragma unroll 4
+    for (int i = 0; i < NN; ++i)
+      if (i != lane) off += fabs(M[i * NN + lane]);
+    dd = fabs(M[lane * NN + lane]) > off;
+  }
+  if (!__all(dd)) return false;
+#pragma unroll 1
+  for (int xo = 0; xo < NN; xo += 64 - NN) wv_solve_dd_pass<NN>(M, X, xo, lane);
+  return true;
+}
+
 // expm(S0) (NN × NN, row-major in LDS slot S0; overwritten) into slot S1, S2 scratch: the Padé
 // scaling-and-squaring of wave_expm (Julia Base 0.3 expm!: degrees 3/5/7/9 below ‖A‖₁ = 2.1,
 // degree 13 with 2^-s scaling above), with the polynomial terms in registers.  Returns true if
@@ -216,7 +282,7 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
   wave_sync();
   bool solved = false;
   if constexpr (2 * NN <= 64) solved = wave_solve_dd<NN>(S0, S1);
-  else if constexpr (NN <= 64) solved = wave_solve_dd2<NN>(S0, S1, S2);
+  else if constexpr (NN <= 64) solved = wv_solve_dd_passes<NN>(S0, S1, lane);
   if (!solved) wave_solve<NN>(S0, S1);
   if (st && lane == 0) st[1] = (long long)__builtin_amdgcn_s_memtime();
   for (int z = 0; z < si; ++z) {
@@ -283,11 +349,18 @@ GPT_HD int wv_dim_lds_dbl(int n, int r, int m) {
   return slots > pre ? slots : pre;
 }
 
+// The V-phase tables (16-bit, wave_tables): [q·D + k] = (k·r + I[q,k])·m, then the run members of
+// every dimension (q with I[q,k] = l, q order, runs in l order), then the D·(r+1) run starts;
+// padded to whole 16-B vectors.
+GPT_HD int wv_table_shorts(int D, int r, int Q) { return (Q * D + D * Q + D * (r + 1) + 7) / 8 * 8; }
+
 // The V-phase workgroup's LDS (doubles): temp of the batch, V (stride m|1), w, y, res, fhat
-// partials and a reduction row.
+// partials, a reduction row and (16-B aligned) the tables.
+GPT_HD int wv_vphase_tab_dbl(int D, int r, int Q, int m) {
+  return (D * r * m + (Q + 1) * (m | 1) + Q + 1 + 2 * 64 + 8 * 64 + 8 + 1) & ~1;
+}
 GPT_HD int wv_vphase_lds_dbl(int D, int r, int Q, int m) {
-  const int shorts = Q * D + D * Q + D * (r + 1);        // temp offsets, run members, run starts
-  return D * r * m + (Q + 1) * (m | 1) + Q + 1 + 2 * 64 + 8 * 64 + 8 + (shorts + 3) / 4;
+  return wv_vphase_tab_dbl(D, r, Q, m) + wv_table_shorts(D, r, Q) / 4;
 }
 
 constexpr int kWvMaxM = 64;            // minibatch rows: one per lane of the V-phase
@@ -324,7 +397,7 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
   double* red = fpart + 8 * 64;
   // 16-bit tables: [q·D + k] = (k·R + I[q,k])·m (< 2^16, wave_supported), the run members
   // (wave_tables), then the run starts
-  unsigned short* toff_l = (unsigned short*)(red + 8);
+  unsigned short* toff_l = (unsigned short*)(wv_sm + wv_vphase_tab_dbl(D, R, Q, m));
   unsigned short* mem_l = toff_l + Q * D;
   unsigned short* seg_l = mem_l + D * Q;
 
@@ -339,11 +412,8 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
     if (tid == 0) w_l[Q] = 0.0;
     for (int i = tid; i < MV; i += 512) V_l[Q * MV + i] = 0.0;
     if (tid < 64) y_l[tid] = tid < Bt ? gptr(Cp->y)[gptr(ord)[tid]] : 0.0;
-    for (int o = tid; o < Q * D; o += 512) {
-      const int q = o / D, k = o - q * D;
-      toff_l[o] = (unsigned short)((k * R + gptr(P.I0)[q + Q * k]) * m);
-    }
-    for (int o = tid; o < D * Q + D * (R + 1); o += 512) mem_l[o] = (unsigned short)gptr(P.wvtab)[o];
+    copy_to_lds<4>((long long*)toff_l, (const long long*)P.wvtab, wv_table_shorts(D, R, Q) / 4, tid,
+                   512);
   }
   __syncthreads();
   // V[q,i] = Π_k temp[k, I[q,k], i] in k order (computeV) and w_q·V partial sums of fhat:
@@ -727,32 +797,46 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
   WSTAMP(srow, 9);
   // ---- tmpU = [U mom]·F row by row (:35 with the two products associated the other way), then
   //      the column normalisation
+  // (a outer: each F row is read from LDS once for the J rows of the lane; the [U mom] values
+  // of four a at a time are in flight)
+#pragma unroll
+  for (int jj = 0; jj < J; ++jj)
+#pragma unroll
+    for (int l = 0; l < R; ++l) u[jj][l] = 0.0;
+#pragma unroll
+  for (int a0 = 0; a0 < 2 * R; a0 += 4) {
+    double x[4][J];
+#pragma unroll
+    for (int da = 0; da < 4; ++da)
+#pragma unroll
+      for (int jj = 0; jj < J; ++jj) {
+        const int a = a0 + da;
+        const double* src = a < R ? Ug + (size_t)n * a : park + (size_t)n * (a - R);
+        x[da][jj] = a < 2 * R ? gptr(src)[jc[jj]] : 0.0;
+      }
+#pragma unroll
+    for (int da = 0; da < 4; ++da) {
+      const int a = a0 + da;
+      if (a < 2 * R) {
+        double f[R];
+#pragma unroll
+        for (int l = 0; l < R; ++l) f[l] = F[a * R + l];
+#pragma unroll
+        for (int jj = 0; jj < J; ++jj) {
+          const double xa = jok[jj] ? x[da][jj] : 0.0;
+#pragma unroll
+          for (int l = 0; l < R; ++l) u[jj][l] = fma(xa, f[l], u[jj][l]);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
   double nrm[R];
 #pragma unroll
-  for (int l = 0; l < R; ++l) nrm[l] = 0.0;
+  for (int l = 0; l < R; ++l) {
+    nrm[l] = 0.0;
 #pragma unroll
-  for (int jj = 0; jj < J; ++jj) {
-    double o[R];
-#pragma unroll
-    for (int l = 0; l < R; ++l) o[l] = 0.0;
-    double x[2 * R];                                     // the row of [U mom], loads in flight
-#pragma unroll
-    for (int a = 0; a < R; ++a) {
-      x[a] = gptr(Ug)[jc[jj] + (size_t)n * a];
-      x[R + a] = gptr(park)[jc[jj] + (size_t)n * a];
-    }
-    __builtin_amdgcn_sched_barrier(0);                   // one row's loads at a time
-#pragma unroll
-    for (int a = 0; a < 2 * R; ++a) {
-      const double xa = jok[jj] ? x[a] : 0.0;
-#pragma unroll
-      for (int l = 0; l < R; ++l) o[l] = fma(xa, F[a * R + l], o[l]);
-    }
-#pragma unroll
-    for (int l = 0; l < R; ++l) {
-      u[jj][l] = o[l];
-      nrm[l] = fma(o[l], o[l], nrm[l]);
-    }
+    for (int jj = 0; jj < J; ++jj) nrm[l] = fma(u[jj][l], u[jj][l], nrm[l]);
   }
   double* nr = S2 + R * R;
   wv_sum_to_lds<R>(nrm, nr, lane);
@@ -815,17 +899,22 @@ bool wave_supported(int n, int D, int r, int Q, int m, bool langevin, bool stief
 
 // D·Q members of every run (core entries q with I[q,k] = l, in q order, runs in l order), then
 // the D·(r+1) run starts.
-void wave_tables(const std::vector<int32_t>& I0, int Q, int D, int r, std::vector<int32_t>& out) {
-  out.assign((size_t)D * Q + (size_t)D * (r + 1), 0);
+void wave_tables(const std::vector<int32_t>& I0, int Q, int D, int r, int m,
+                 std::vector<uint16_t>& out) {
+  out.assign((size_t)wv_table_shorts(D, r, Q), 0);
+  for (int q = 0; q < Q; ++q)
+    for (int k = 0; k < D; ++k)
+      out[(size_t)q * D + k] = (uint16_t)((k * r + I0[q + (size_t)Q * k]) * m);
+  uint16_t* mem = out.data() + (size_t)Q * D;
   for (int k = 0; k < D; ++k) {
     int pos = 0;
-    int32_t* seg = out.data() + (size_t)D * Q + (size_t)k * (r + 1);
+    uint16_t* seg = mem + (size_t)D * Q + (size_t)k * (r + 1);
     for (int l = 0; l < r; ++l) {
-      seg[l] = pos;
+      seg[l] = (uint16_t)pos;
       for (int q = 0; q < Q; ++q)
-        if (I0[q + (size_t)Q * k] == l) out[(size_t)k * Q + pos++] = q;
+        if (I0[q + (size_t)Q * k] == l) mem[(size_t)k * Q + pos++] = (uint16_t)q;
     }
-    seg[r] = pos;
+    seg[r] = (uint16_t)pos;
   }
 }
 
