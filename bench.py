@@ -304,6 +304,141 @@ def compose_line(v):
     }
 
 
+ML_CONFIG = dict(signal_var=0.8, sigma_u=0.1, sigma_w=1.0, m=100, epsw=1e-4, epsU=1e-6, a=0.5,
+                 b=0.25, c=0.5, burnin=0, maxepoch=200, param_seed=17)
+
+
+def movielens_bytes_per_step(ud, md, m, r):
+    """Algorithmic HBM bytes of one GPT_fullw_sideinfo minibatch step (100k_movielensExperiment.jl
+    :455-507; cf_epoch_kernel): the batch's (user, movie, rating) triples, the U / V rows and
+    side-feature rows its sums read (mean feature count per user / movie), the gradient rows
+    written (at most 2m + D1 + D2), and the dense move of every row of U and V (the prior term
+    moves all rows: read M and G, write M and zero G)."""
+    n1, D1 = ud.shape
+    n2, D2 = md.shape
+    fu, fv = float(ud.sum(axis=1).mean()), float(md.sum(axis=1).mean())
+    gather = m * (4 + 4 + 8 + 4) + 8 * m * r * (2 + fu + fv)
+    grads = 8 * r * (2 * m + D1 + D2)
+    move = 4 * 8 * r * (n1 + D1 + n2 + D2)
+    return gather + grads + move
+
+
+def movielens_cpu_baseline(fold1, w0, cfg, epochs=1):
+    """The numpy restatement of GPT_fullw_sideinfo (oracle/movielens_ref.py, 1 core) on fold 1
+    for ``epochs`` epochs of the live configuration."""
+    from oracle import movielens_ref as M
+    tr, te, ud, md, mu, sd = fold1
+    t0 = time.perf_counter()
+    M.GPT_fullw_sideinfo(tr, ud, md, te, cfg["signal_var"], cfg["sigma_u"], cfg["sigma_w"], w0,
+                         cfg["m"], cfg["epsw"], cfg["epsU"], cfg["a"], cfg["b"], cfg["c"], 0,
+                         epochs, cfg["param_seed"], mu, sd)
+    dt = time.perf_counter() - t0
+    steps = epochs * -(-tr.shape[0] // cfg["m"])
+    return dict(value=steps / dt, unit="fold-steps/s (1 fold, 1 core)", cores=1, kind="port",
+                sample="oracle/movielens_ref.py (numpy restatement of "
+                       "100k_movielensExperiment.jl:409-551) on fold 1, %d epoch(s) = %d minibatch "
+                       "steps plus the per-epoch train / test evaluation, in %.1f s"
+                       % (epochs, steps, dt))
+
+
+def movielens_main(args):
+    """bench.py --workload movielens: the live experiment of 100k_movielensExperiment.jl:723-739
+    (GPT_fullw_sideinfo on the 5 ml-100k folds, SGD, σ_u = 0.1, σ² = 0.8, εU = 1e-6, εw = 1e-4,
+    a, b, c = 0.5, 0.25, 0.5, m = 100, 200 epochs, param_seed 17) at BASELINE config 5's r = 20
+    (the script runs r = 15; --r).  The folds run as sibling chains of one cf_epoch_kernel launch
+    per epoch (gpt_cf_fullw_sideinfo_folds); value = minibatch steps summed over the folds / wall
+    time of the whole call (host evaluation, stores and early stop included); roofline from the
+    device time of the epoch launches (hipEvents inside the library, gpt_cf_last_timing).  N > 1:
+    every rank runs the experiment with its own param_seed (replicas, no collective)."""
+    import torch
+    import torch.distributed as dist
+    from gpt_amd import movielens
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = dict(ML_CONFIG)
+    r = args.r if args.r is not None else 20
+    epochs = args.epochs
+    cfg["param_seed"] += rank
+    d = np.load(os.path.join(ROOT, "tests", "golden", "ml100k.npz"))
+    folds = [movielens.fold(d, i) for i in range(1, 6)]
+    trs, tes = [f[0] for f in folds], [f[1] for f in folds]
+    ud, md = folds[0][2], folds[0][3]
+    mus, sds = [f[4] for f in folds], [f[5] for f in folds]
+    w0 = cfg["sigma_w"] * np.random.default_rng(cfg["param_seed"]).standard_normal((r, r))
+
+    def run(E):
+        return movielens.GPT_fullw_sideinfo_folds(
+            trs, ud, md, tes, cfg["signal_var"], cfg["sigma_u"], cfg["sigma_w"], w0, cfg["m"],
+            cfg["epsw"], cfg["epsU"], cfg["a"], cfg["b"], cfg["c"], cfg["burnin"], E,
+            cfg["param_seed"], mus, sds)
+
+    run(max(1, args.warmup_epochs))                  # warm-up: kernels loaded, clocks up
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = run(epochs)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    tm = movielens.last_timing()
+    dt = max_over_ranks(wall, dev)
+    steps_all = gather_over_ranks(float(tm["fold_steps"]), dev)
+    value = sum(steps_all) / dt
+    mins = [float(o[5].min()) for o in outs]
+    bstep = movielens_bytes_per_step(ud, md, cfg["m"], r)
+    ep_us = 1e3 * tm["epoch_ms"] / max(tm["epochs"], 1)
+    steps_per_launch = tm["fold_steps"] / max(tm["epochs"], 1)
+    achieved = bstep * steps_per_launch / (ep_us * 1e-6) / 1e9
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = movielens_cpu_baseline(folds[0], w0, cfg)
+    if rank == 0:
+        nb = -(-trs[0].shape[0] // cfg["m"])
+        out = {
+            "metric": "GPT_fullw_sideinfo minibatch steps/sec + test RMSE (100k_movielensExperiment.jl, "
+                      "5 folds, r=%d)" % r,
+            "value": value, "unit": "fold-steps/s", "n_gpus": world, "steps": int(tm["fold_steps"]),
+            "warmup": int(max(1, args.warmup_epochs)) * nb * len(folds),
+            "ms_per_step": 1e3 * dt / max(1, tm["fold_steps"] / len(folds)),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "ml-100k u1..u5 base/test + u.user / u.item side information "
+                    "(tests/golden/ml100k.npz), ratings standardised per fold",
+            "config": {"workload": "GPT_fullw_sideinfo, 5 folds as sibling chains (SGD: "
+                                   "langevin = stiefel = false, :733-736)",
+                       "r": r, "epochs": epochs, "folds": len(folds), "Ntrain": int(trs[0].shape[0]),
+                       "Ntest": int(tes[0].shape[0]), "users": int(ud.shape[0]), "movies": int(md.shape[0]),
+                       "D1": int(ud.shape[1]), "D2": int(md.shape[1]), **cfg,
+                       "parallelism": "folds%dx%d" % (len(folds), world)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "cf_epoch_kernel<%d>" % r,
+                         "kernel_us": ep_us, "kernel_us_note": "per epoch launch (every live fold's "
+                         "%d minibatch steps), hipEvents inside gpt_cf_fullw_sideinfo_folds" % nb,
+                         "eval_kernel_us": 1e3 * tm["eval_ms"] / max(tm["epochs"], 1),
+                         "algorithmic_bytes_per_step": bstep,
+                         "algorithmic_bytes_per_launch": bstep * steps_per_launch,
+                         "device_fraction_of_wall": (tm["epoch_ms"] + tm["eval_ms"]) / (1e3 * wall)},
+            "cpu_baseline": cpu,
+            "test_rmse": float(np.mean(mins)),
+            "test_rmse_note": "meantestRMSE of :735-737: mean over the folds of each fold's minimum "
+                              "per-epoch test RMSE (rating units, predictions cut off to [1, 5])",
+            "quality": {"min_test_rmse_per_fold": mins,
+                        "epochs_run_per_fold": [int((o[4] > 0).sum()) for o in outs],
+                        "final_train_rmse_per_fold": [float(o[4][o[4] > 0][-1]) if (o[4] > 0).any()
+                                                      else None for o in outs]},
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def gather_over_ranks(x, device=None):
     """[x of rank 0, .., x of rank N-1] (every rank gets the list)."""
     import torch
@@ -325,8 +460,11 @@ def main():
                     help="independent chains per GPU (0: one per CU for the chain engine, two at "
                          "D <= 4; CUs // (D+1) for the grid engine, D+1 workgroups per chain)")
     ap.add_argument("--engine", default="auto", choices=["auto", "grid", "chain", "wave"])
-    ap.add_argument("--workload", default="kin40k", choices=sorted(WORKLOADS),
-                    help="kin40k (BASELINE configs 3/4, the metric's workload) or powerplant (config 2)")
+    ap.add_argument("--workload", default="kin40k", choices=sorted(WORKLOADS) + ["movielens"],
+                    help="kin40k (BASELINE configs 3/4, the metric's workload), kin40k_ref "
+                         "(kin40kExperiment.jl's n=150, r=20), powerplant (config 2) or movielens "
+                         "(config 5: GPT_fullw_sideinfo over the 5 ml-100k folds)")
+    ap.add_argument("--warmup-epochs", type=int, default=2, help="movielens: warm-up call's epochs")
     ap.add_argument("--n", type=int, default=None, help="default: the workload's (500 / 150)")
     ap.add_argument("--D", type=int, default=None, help="default: the workload's D (8 / 4)")
     ap.add_argument("--r", type=int, default=None, help="default: the workload's (5 / 20)")
@@ -355,6 +493,8 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: re-run under torchrun before any HIP call in this process
         raise SystemExit(self_launch(sys.argv[1:], args.gpus))
+    if args.workload == "movielens":
+        return movielens_main(args)
     loader, wD, wm, wls, sigma_rbf, wsv, wdesc, wn, wr, wew, weu = WORKLOADS[args.workload]
     for k_, v_ in (("n", wn), ("r", wr), ("epsw", wew), ("epsU", weu)):
         if getattr(args, k_) is None:

@@ -1576,6 +1576,11 @@ struct CfFold {
 // permutation; every fold has the same number of training ratings.  fixw keeps w at w_init
 // (w_store may then be null); D1 = D2 = 0 with a = 1, b = c = 0 is the model without side
 // information.
+// Device time of the last CF SGD run on this thread (gpt_cf_last_timing): hipEvents around each
+// epoch / eval launch, read after the per-epoch status copy that synchronises anyway.
+struct CfTiming { double epoch_ms, eval_ms; int64_t epochs, evals, fold_steps; };
+static thread_local CfTiming g_cf_timing{};
+
 static int cf_sgd_run(
     const char* name, std::vector<CfFold>& folds, const double* UserData, int64_t n1, int64_t D1,
     const double* MovieData, int64_t n2, int64_t D2, double signal_var, double sigma_u,
@@ -1699,11 +1704,27 @@ static int cf_sgd_run(
   std::vector<int> testcounter(F, 0);
   int counter = 0, nlive = F;
   const int32_t stopped = 2;                         // skips the fold in later launches
+  struct Events {
+    hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+    ~Events() { for (auto x : e) if (x) (void)hipEventDestroy(x); }
+  } evs;
+  for (auto& x : evs.e) HIPCHK(hipEventCreate(&x));
+  g_cf_timing = CfTiming{};
   for (int64_t epoch = 1; epoch <= burnin + maxepoch && nlive > 0; ++epoch) {
     host_randperm((int)N, seed, (int)(epoch - 1), perm.data());
     HIPCHK(hipMemcpy(d_perm.p, perm.data(), 4 * N, hipMemcpyHostToDevice));
+    HIPCHK(hipEventRecord(evs.e[0], nullptr));
     hipError_t e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, (epoch - 1) * nbatch, nbatch, nullptr);
     if (e != hipSuccess) return hip_fail(e, "cf epoch kernel");
+    HIPCHK(hipEventRecord(evs.e[1], nullptr));
+    HIPCHK(hipEventSynchronize(evs.e[1]));
+    {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, evs.e[0], evs.e[1]));
+      g_cf_timing.epoch_ms += ms;
+      g_cf_timing.epochs += 1;
+      g_cf_timing.fold_steps += (int64_t)nlive * nbatch;
+    }
     for (int f = 0; f < F; ++f) {
       if (!live[f]) continue;
       int32_t bad = 0;
@@ -1720,8 +1741,17 @@ static int cf_sgd_run(
     if (epoch > burnin && nlive > 0) {
       const int64_t s2 = epoch - burnin - 1;
       if (!avg) counter = 0;
+      HIPCHK(hipEventRecord(evs.e[2], nullptr));
       e = launch_cf_eval(P, d_ch.as<CfChain>(), F, nmax, counter, nullptr);
       if (e != hipSuccess) return hip_fail(e, "cf eval kernel");
+      HIPCHK(hipEventRecord(evs.e[3], nullptr));
+      HIPCHK(hipEventSynchronize(evs.e[3]));
+      {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, evs.e[2], evs.e[3]));
+        g_cf_timing.eval_ms += ms;
+        g_cf_timing.evals += 1;
+      }
       for (int f = 0; f < F; ++f) {
         if (!live[f]) continue;
         CfFold& fd = folds[f];
@@ -1814,6 +1844,18 @@ extern "C" int gpt_cf_fullw_sideinfo_folds(
   if (status)
     for (int64_t f = 0; f < F; ++f) status[f] = folds[f].status;
   return rc;
+}
+
+extern "C" int gpt_cf_last_timing(double* epoch_ms, double* eval_ms, int64_t* epochs,
+                                   int64_t* fold_steps) {
+  if (!epoch_ms || !eval_ms || !epochs || !fold_steps) {
+    set_error("gpt_cf_last_timing: null output"); return GPT_ERR_BAD_DIMS;
+  }
+  *epoch_ms = g_cf_timing.epoch_ms;
+  *eval_ms = g_cf_timing.eval_ms;
+  *epochs = g_cf_timing.epochs;
+  *fold_steps = g_cf_timing.fold_steps;
+  return GPT_OK;
 }
 
 extern "C" int gpt_cf_fixw_sideinfo(

@@ -212,6 +212,15 @@ def GPT_fixw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u,
     return U_store, V_store, tps, trm, tsm
 
 
+def last_timing():
+    """Device time of the last CF SGD / SGLD call on this thread (gpt_cf_last_timing): dict with
+    epoch_ms (cf_epoch_kernel launches), eval_ms (cf_eval_kernel), epochs and fold_steps."""
+    em, vm = C.c_double(), C.c_double()
+    ne, fs = C.c_int64(), C.c_int64()
+    check(lib().gpt_cf_last_timing(C.byref(em), C.byref(vm), C.byref(ne), C.byref(fs)))
+    return dict(epoch_ms=em.value, eval_ms=vm.value, epochs=ne.value, fold_steps=fs.value)
+
+
 def GPT_fullw_sideinfo_folds(Ratings, UserData, MovieData, Ratingtests, signal_var, sigma_u,
                              sigma_w, w_init, m, epsw, epsU, a, b, c, burnin, maxepoch, param_seed,
                              ytrainMeans, ytrainStds, langevin=False, stiefel=False, avg=False):

@@ -304,6 +304,13 @@ int gpt_cf_fullw_sideinfo_folds(int64_t F, const double* const* Rating, const in
                                 double* const* V_store, double* const* testpred_store,
                                 double* const* trainRMSE, double* const* testRMSE, int32_t* status);
 
+/* Device time of the last CF SGD / SGLD run (any gpt_cf_* SGD entry, fixw / sideinfo / folds)
+ * on the calling thread: hipEvents around each epoch launch (cf_epoch_kernel, every live fold's
+ * minibatch steps of one epoch) and each evaluation launch (cf_eval_kernel); epochs = epoch
+ * launches, fold_steps = minibatch steps summed over the folds live in each launch.  No
+ * reference counterpart (measurement, bench.py --workload movielens). */
+int gpt_cf_last_timing(double* epoch_ms, double* eval_ms, int64_t* epochs, int64_t* fold_steps);
+
 /* The other SGD / SGLD variants of the CF model (same Rating / Ratingtest / output conventions
  * as gpt_cf_fullw_sideinfo; the NaN bail-out zeroes the parameter stores):
  *   GPT_fixw_sideinfo(Rating,UserData,MovieData,Ratingtest,signal_var,sigma_u,w,m,epsU,a,b,c,
