@@ -43,7 +43,7 @@ __device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int w
   if (!P.stiefel) {
     const double su2 = P.sigma_u * P.sigma_u;
     for (int o = tid; o < rows * (RE / 2); o += kCfNT) {
-      const int row = o / (RE / 2), lp = o - row * (RE / 2);
+      const int lp = o / rows, row = o - lp * rows;       // consecutive rows: coalesced
       double z[2] = {0.0, 0.0};
       if (P.langevin)
         normal_pair(P.seed, (uint32_t)((2 * lp + RE * row) >> 1), st, kCfUVNoise, (uint32_t)which,
@@ -74,7 +74,7 @@ __device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int w
   double* nr = F + NN * R;          // R
   int* flag = (int*)(nr + R);
   for (int o = tid; o < rows * (RE / 2); o += kCfNT) {
-    const int row = o / (RE / 2), lp = o - row * (RE / 2);
+    const int lp = o / rows, row = o - lp * rows;       // consecutive rows: coalesced
     double z[2] = {0.0, 0.0};
     if (P.langevin)
       normal_pair(P.seed, (uint32_t)((2 * lp + RE * row) >> 1), st, kCfUVNoise, (uint32_t)which,
@@ -197,8 +197,17 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
   double* tU = sV + (size_t)m * R;              // m × R   sumU·w
   double* tV = tU + (size_t)m * R;              // m × R   w·sumVᵀ
   double* er = tV + (size_t)m * R;              // m       rating, then residual
-  int* us = (int*)(er + m);                     // m
+  // side-information bitmasks of the batch's users / movies (D1, D2 <= 64: the feature rows of a
+  // rating without walking the CSR lists in global memory every time)
+  uint64_t* umk = (uint64_t*)(er + m);          // m
+  uint64_t* vmk = umk + m;                      // m
+  int* us = (int*)(vmk + m);                    // m
   int* ms = us + m;                             // m
+  // per batch position ii of each side: (next position with the same user / movie) + 1, or 0,
+  // with bit 16 set when ii is that id's first position in the batch (its gradient row's owner)
+  int* unx = ms + m;                            // m
+  int* vnx = unx + m;                           // m
+  const bool masks = P.D1 <= 64 && P.D2 <= 64;
   // Stiefel scratch of the U / V moves: aliases the batch buffers (sU .. ms), which are dead from
   // the barrier before the moves until the next batch reloads them (r = 20 fits 160 KB this way)
   double* scr = sU;
@@ -216,16 +225,50 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       er[ii] = C.tr_rating[idx];
     }
     __syncthreads();
-    // sumU = U[user,:] + b·sum(U[uidx,:],1), sumV likewise (:462)
+    // per (side, ii): the feature bitmask, the first-occurrence flag and the next occurrence
+    for (int o = tid; o < 2 * B; o += kCfNT) {
+      const int side = o >= B ? 1 : 0, ii = o - side * B;
+      const int* ids = side ? ms : us;
+      const int id = ids[ii];
+      if (masks) {
+        const int32_t* ptr = side ? P.vptr : P.uptr;
+        const int32_t* fe = side ? P.vfe : P.ufe;
+        const int base = side ? P.n2 : P.n1;
+        uint64_t mk = 0;
+        for (int z = ptr[id]; z < ptr[id + 1]; ++z) mk |= 1ull << (fe[z] - base);
+        (side ? vmk : umk)[ii] = mk;
+      }
+      bool first = true;
+      int nx = -1;
+      for (int z = 0; z < B; ++z) {
+        const bool same = ids[z] == id;
+        first &= !(same && z < ii);
+        if (same && z > ii && nx < 0) nx = z;
+      }
+      (side ? vnx : unx)[ii] = (nx + 1) | (first ? 1 << 16 : 0);
+    }
+    __syncthreads();
+    // sumU = U[user,:] + b·sum(U[uidx,:],1), sumV likewise (:462); the feature rows in ascending
+    // order (find(UserData[i,:]), the CSR order)
     for (int o = tid; o < 2 * B * R; o += kCfNT) {
       const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
       const double* M = side ? C.V : C.U;
       const int rows = side ? P.rowsV : P.rowsU;
       const int id = side ? ms[ii] : us[ii];
-      const int32_t* ptr = side ? P.vptr : P.uptr;
-      const int32_t* fe = side ? P.vfe : P.ufe;
       double f = 0.0;
-      for (int z = ptr[id]; z < ptr[id + 1]; ++z) f += gptr(M)[fe[z] + (size_t)rows * l];
+      if (masks) {
+        const int base = side ? P.n2 : P.n1;
+        uint64_t mk = (side ? vmk : umk)[ii];
+        while (mk) {
+          const int fb = __ffsll((long long)mk) - 1;
+          mk &= mk - 1;
+          f += gptr(M)[base + fb + (size_t)rows * l];
+        }
+      } else {
+        const int32_t* ptr = side ? P.vptr : P.uptr;
+        const int32_t* fe = side ? P.vfe : P.ufe;
+        for (int z = ptr[id]; z < ptr[id + 1]; ++z) f += gptr(M)[fe[z] + (size_t)rows * l];
+      }
       const double v = gptr(M)[id + (size_t)rows * l] + (side ? P.c : P.b) * f;
       (side ? sV : sU)[ii * R + l] = v;
     }
@@ -264,17 +307,15 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     }
     // gradient rows in rating order (:467-471): the first rating of a user / movie in the batch
     // sums its row; feature rows sum over the ratings whose user / movie carries them
+    // (the same-id positions of a first occurrence are walked through the next links, ascending)
     for (int o = tid; o < 2 * B * R; o += kCfNT) {
       const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
-      const int* ids = side ? ms : us;
-      const int id = ids[ii];
-      bool first = true;
-      for (int z = 0; z < ii; ++z) first &= ids[z] != id;
-      if (!first) continue;
+      const int* nxl = side ? vnx : unx;
+      if (!(nxl[ii] >> 16)) continue;
+      const int id = (side ? ms : us)[ii];
       const double* T = side ? tU : tV;     // Vtemp = e·(sumU*w), Utemp = e·(sumV*w')
       double g = 0.0;
-      for (int z = ii; z < B; ++z)
-        if (ids[z] == id) g += P.a * (er[z] * T[z * R + l]) * is2;
+      for (int z = ii; z >= 0; z = (nxl[z] & 0xFFFF) - 1) g += P.a * (er[z] * T[z * R + l]) * is2;
       double* G = side ? C.GV : C.GU;
       gptr_w(G)[id + (size_t)(side ? P.rowsV : P.rowsU) * l] = g * cN;
     }
@@ -282,18 +323,24 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       const int side = o >= P.D1 * R ? 1 : 0;
       const int x = side ? o - P.D1 * R : o, f = x / R, l = x - f * R;
       const int* ids = side ? ms : us;
-      const int32_t* ptr = side ? P.vptr : P.uptr;
-      const int32_t* fe = side ? P.vfe : P.ufe;
       const int row = (side ? P.n2 : P.n1) + f;
       const double ab = P.a * (side ? P.c : P.b);
       const double* T = side ? tU : tV;
       double g = 0.0;
       bool hit = false;
-      for (int z = 0; z < B; ++z) {
-        const int id = ids[z];
-        bool has = false;
-        for (int q = ptr[id]; q < ptr[id + 1]; ++q) has |= fe[q] == row;
-        if (has) { g += ab * (er[z] * T[z * R + l]) * is2; hit = true; }
+      if (masks) {
+        const uint64_t* mk = side ? vmk : umk;
+        for (int z = 0; z < B; ++z)
+          if ((mk[z] >> f) & 1ull) { g += ab * (er[z] * T[z * R + l]) * is2; hit = true; }
+      } else {
+        const int32_t* ptr = side ? P.vptr : P.uptr;
+        const int32_t* fe = side ? P.vfe : P.ufe;
+        for (int z = 0; z < B; ++z) {
+          const int id = ids[z];
+          bool has = false;
+          for (int q = ptr[id]; q < ptr[id + 1]; ++q) has |= fe[q] == row;
+          if (has) { g += ab * (er[z] * T[z * R + l]) * is2; hit = true; }
+        }
       }
       if (hit) gptr_w(side ? C.GV : C.GU)[row + (size_t)(side ? P.rowsV : P.rowsU) * l] = g * cN;
     }
@@ -505,7 +552,8 @@ hipError_t launch_cfg_kron(int r, const double* U, int n1, const double* V, int 
 }
 
 size_t cf_lds_bytes(int r, int m) {
-  const size_t base = 8 * (2 * (size_t)r * r + 4 * (size_t)m * r + m) + 4 * (2 * (size_t)m + 2);
+  const size_t base = 8 * (2 * (size_t)r * r + 4 * (size_t)m * r + m) + 16 * (size_t)m +
+                      4 * (4 * (size_t)m + 2);
   const size_t nn = 2 * (size_t)r;
   const size_t stf = 8 * (3 * (size_t)r * r + 7 * nn * nn + 7 * (size_t)r * r + nn * r + r) + 16;
   const size_t moves = 8 * 2 * (size_t)r * r + stf;      // w | wn | Stiefel scratch over the batch

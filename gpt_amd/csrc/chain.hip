@@ -72,7 +72,7 @@ struct ChainLds {
   // stays under 80 KB for two chains per CU and draws its angles by polynomial)
   static constexpr int o_tab = al16c(o_un + 8 * (L_dbl > x_dbl * WV ? L_dbl : x_dbl * WV));
   static constexpr bool tab = WV == kChainDMax;
-  static constexpr int bytes = al16c(o_tab + (tab ? 8 * 512 : 0));
+  static constexpr int bytes = al16c(o_tab + (tab ? 8 * 64 : 0));
 };
 
 // Timeline of every workgroup in P.stamps (gpt_sgld_session_timeline; kTimeline slots per block).

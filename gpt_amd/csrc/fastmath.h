@@ -121,6 +121,31 @@ GPT_HD void fm_sincos_tab(uint32_t x, const TP* tab, double& sn, double& cs, CP 
   cs = fma(ct, cp, -(st * sp));
 }
 
+// fm_sincos_tab with the 256-entry table factored into two 16-entry ones: tab[2j], tab[2j + 1] =
+// (sin, cos)(2πj/16) and tab[32 + 2j], tab[33 + 2j] = (sin, cos)(2πj/256), j < 16, so i = 16·ih + il
+// takes the angle sum of entries ih and il first.  Each 16-entry table is 256 contiguous bytes —
+// every LDS bank once — so the per-lane 16-B reads of a wave never conflict (lanes with the same
+// entry share it; the 256-entry table's random rows cost ~3 passes per read).  Within 3 ulp of
+// fm_sincos_2pi_c.
+template <class CP, class TP>
+GPT_HD void fm_sincos_tab2(uint32_t x, const TP* tab, double& sn, double& cs, CP c) {
+  const unsigned ih = x >> 28, il = (x >> 24) & 15u;
+  const double ph = ((double)(x & 0xFFFFFFu) + 0.5) * c[23];
+  const double z = ph * ph;
+  double ts = fma(z, c[26], c[25]);
+  ts = fma(z, ts, c[24]);
+  const double sp = fma(ph * z, ts, ph);
+  double tc = fma(z, c[30], c[29]);
+  tc = fma(z, tc, c[28]);
+  tc = fma(z, tc, c[27]);
+  const double cp = fma(z, tc, 1.0);
+  const double s1 = tab[2 * ih], c1 = tab[2 * ih + 1];
+  const double s2 = tab[32 + 2 * il], c2 = tab[33 + 2 * il];
+  const double st = fma(s1, c2, c1 * s2), ct = fma(c1, c2, -(s1 * s2));
+  sn = fma(st, cp, ct * sp);
+  cs = fma(ct, cp, -(st * sp));
+}
+
 // √x for finite normal x > 0 (the Box–Muller radius: x = −2 ln u in [2e-10, 46]): on the device
 // the hardware rsq refined by two Newton steps (the refinement of the library expansion without
 // its denormal scaling and class checks).

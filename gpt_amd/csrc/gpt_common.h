@@ -118,8 +118,8 @@ __device__ __forceinline__ void normal_quad(uint64_t seed, uint32_t c0, uint32_t
   }
 }
 
-// normal_quad with the angles from fm_sincos_tab (table in LDS, filled by sincos_tab_fill): the
-// same streams to within 2 ulp
+// normal_quad with the angles from fm_sincos_tab2 (two 16-entry tables in LDS, filled by
+// sincos_tab_fill): the same streams to within 3 ulp
 template <int NZ>
 __device__ __forceinline__ void normal_quad_tab(uint64_t seed, uint32_t c0, uint32_t c1,
                                                 uint32_t c2, uint32_t c3, const double* tab,
@@ -129,24 +129,25 @@ __device__ __forceinline__ void normal_quad_tab(uint64_t seed, uint32_t c0, uint
   {
     const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.x), c));
     double sn, cs;
-    fm_sincos_tab(x.y, tab, sn, cs, c);
+    fm_sincos_tab2(x.y, tab, sn, cs, c);
     z[0] = rad * cs;
     z[1] = rad * sn;
   }
   if constexpr (NZ == 4) {
     const double rad = fm_sqrt_pos(-2.0 * fm_log_c(u32u(x.z), c));
     double sn, cs;
-    fm_sincos_tab(x.w, tab, sn, cs, c);
+    fm_sincos_tab2(x.w, tab, sn, cs, c);
     z[2] = rad * cs;
     z[3] = rad * sn;
   }
 }
-// (sin, cos)(2πi/256) for i < 256 into tab[2i], tab[2i + 1]
+// (sin, cos)(2πj/16) into tab[2j], tab[2j + 1] and (sin, cos)(2πj/256) into tab[32 + 2j],
+// tab[33 + 2j], j < 16 (fm_sincos_tab2)
 __device__ __forceinline__ void sincos_tab_fill(double* tab, int tid, int nth) {
   const auto c = fm_coef();
-  for (int i = tid; i < 256; i += nth) {
+  for (int i = tid; i < 32; i += nth) {
     double sn, cs;
-    fm_sincos_2pi_c((double)i * (1.0 / 256.0), sn, cs, c);
+    fm_sincos_2pi_c((double)(i & 15) * (i < 16 ? 1.0 / 16.0 : 1.0 / 256.0), sn, cs, c);
     tab[2 * i] = sn;
     tab[2 * i + 1] = cs;
   }
