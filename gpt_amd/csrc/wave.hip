@@ -137,7 +137,7 @@ __device__ __forceinline__ void wv_solve_dd_pass(const double* M, double* X, int
 }
 
 template <int NN>
-__device__ __forceinline__ bool wv_solve_dd_passes(const double* M, double* X, int lane) {
+__device__ __forceinline__ bool wv_solve_dd_passes(const double* M, double* X, int lane, int ncols) {
   static_assert(NN > 32 && NN < 64, "one X column per lane beside M's");
   bool dd = true;
   if (lane < NN) {
@@ -149,17 +149,21 @@ __device__ __forceinline__ bool wv_solve_dd_passes(const double* M, double* X, i
   }
   if (!__all(dd)) return false;
 #pragma unroll 1
-  for (int xo = 0; xo < NN; xo += 64 - NN) wv_solve_dd_pass<NN>(M, X, xo, lane);
+  for (int xo = 0; xo < ncols; xo += 64 - NN) wv_solve_dd_pass<NN>(M, X, xo, lane);
   return true;
 }
 
 // expm(S0) (NN × NN, row-major in LDS slot S0; overwritten) into slot S1, S2 scratch: the Padé
 // scaling-and-squaring of wave_expm (Julia Base 0.3 expm!: degrees 3/5/7/9 below ‖A‖₁ = 2.1,
 // degree 13 with 2^-s scaling above), with the polynomial terms in registers.  Returns true if
-// the result holds a NaN (the geod bail-out, GPT_SGLD.jl:23-26).
+// the result holds a NaN (the geod bail-out, GPT_SGLD.jl:23-26).  ncols < NN: only columns
+// [0, ncols) of the result are wanted (geod reads E[:, 1:r]); without squarings (‖A‖₁ <= 5.4) the
+// solve then takes those right-hand sides only — each column's operations are the full solve's,
+// so they are the same doubles — and the NaN check covers them (with squarings every column is
+// solved and checked).
 template <int NN>
 __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int lane,
-                                        long long* st = nullptr) {
+                                        long long* st = nullptr, int ncols = NN) {
   constexpr int BS = Blk<NN>::BS;
   double cs = 0.0;
   if (lane < NN) {
@@ -281,8 +285,9 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
   }
   wave_sync();
   bool solved = false;
+  const int nc = si > 0 ? NN : ncols;
   if constexpr (2 * NN <= 64) solved = wave_solve_dd<NN>(S0, S1);
-  else if constexpr (NN <= 64) solved = wv_solve_dd_passes<NN>(S0, S1, lane);
+  else if constexpr (NN <= 64) solved = wv_solve_dd_passes<NN>(S0, S1, lane, nc);
   if (!solved) wave_solve<NN>(S0, S1);
   if (st && lane == 0) st[1] = (long long)__builtin_amdgcn_s_memtime();
   for (int z = 0; z < si; ++z) {
@@ -293,7 +298,7 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
     wave_sync();
   }
   bool bad = false;
-  for (int o = lane; o < NN * NN; o += 64) bad |= (S1[o] != S1[o]);
+  for (int o = lane; o < NN * NN; o += 64) bad |= (o % NN < nc) && (S1[o] != S1[o]);
   return __any(bad);
 }
 
@@ -772,7 +777,8 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
       S0[o] = tt * v;
     }
     wave_sync();
-    bad = wv_expm<NN>(S0, S1, S2, lane, P.stamps ? P.stamps + (size_t)srow * kStamps + 12 : nullptr);
+    bad = wv_expm<NN>(S0, S1, S2, lane, P.stamps ? P.stamps + (size_t)srow * kStamps + 12 : nullptr,
+                      R);
   }
   WSTAMP(srow, 8);
   // F = E[:, 1:r]·expm(−tA) (2r × r) into slot 0; expm(−tA) back to LDS at slot 2
