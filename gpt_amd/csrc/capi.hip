@@ -787,6 +787,24 @@ extern "C" int gpt_debug_expm(int32_t nn, int32_t count, int32_t mode, const dou
   return GPT_OK;
 }
 
+extern "C" int gpt_debug_expm_stamps(int32_t nn, int32_t count, const double* A, int64_t* stamps) {
+  if (count < 1 || !A || !stamps) { set_error("bad arguments"); return GPT_ERR_BAD_DIMS; }
+  const size_t b = 8 * (size_t)nn * nn * count;
+  DevMem dA, dE, dB, dS;
+  HIPCHK(dA.alloc(b));
+  HIPCHK(dE.alloc(b));
+  HIPCHK(dB.alloc(4 * (size_t)count));
+  HIPCHK(dS.alloc(32 * (size_t)count));
+  HIPCHK(hipMemcpy(dA.p, A, b, hipMemcpyHostToDevice));
+  hipError_t e = launch_expm_check(nn, count, dA.as<double>(), dE.as<double>(), dB.as<int32_t>(), 2,
+                                   nullptr, dS.as<long long>());
+  if (e == hipErrorInvalidValue) { set_error("nn not instantiated"); return GPT_ERR_BAD_DIMS; }
+  HIPCHK(e);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(stamps, dS.p, 32 * (size_t)count, hipMemcpyDeviceToHost));
+  return GPT_OK;
+}
+
 extern "C" int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, int64_t* out,
                                          double* event_us) {
   if (!s || !out) { set_error("null argument"); return GPT_ERR_BAD_DIMS; }

@@ -205,7 +205,7 @@ size_t wv_vphase_lds_bytes(int D, int r, int Q, int m);
 hipError_t launch_wave(const StepParams& P, const ChainDesc* chains, int nchains,
                        const long long* tbase, int t_local, bool init, hipStream_t st);
 hipError_t launch_expm_check(int nn, int count, const double* A, double* E, int32_t* bad, int mode,
-                             hipStream_t st);
+                             hipStream_t st, long long* stamps = nullptr);
 
 
 hipError_t launch_pred_x(const double* w, const double* U, const int32_t* I0, const double* X,

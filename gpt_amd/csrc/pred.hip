@@ -640,10 +640,6 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
   if (e != hipSuccess) return e;
   int32_t* offs = (int32_t*)((char*)T + tbytes);
   int32_t* offp = offs + (size_t)Q * D;
-  hipLaunchKernelGGL(pred_offs_kernel, dim3((Q * D + 255) / 256), dim3(256), 0, st, I0, Q, D, r,
-                     offs);
-  hipLaunchKernelGGL(pred_pair_offs_kernel, dim3((Q * NTp + 255) / 256), dim3(256), 0, st, I0, Q,
-                     D, r, offp);
   const size_t rlds = 8 * (size_t)D * r * 64;
   // V-phase variant: "pairs" (default where the tables fit: ⌈D/2⌉ ≤ 8 and ≤ 96 KB), "rows", "tile"
   const int vmode = [] {
@@ -662,6 +658,16 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     if (timing) (void)hipEventRecord(ev[0], st);
     e = launch_pred_gemm(Us, phitest, n, D, r, Ntest, Sc, T, st);
     if (e != hipSuccess) break;
+    if (s0 == 0) {
+      // the V-phase's offset table, launched behind the first GEMM (its launch latency then hides
+      // under the GEMM instead of delaying it)
+      if (pairs)
+        hipLaunchKernelGGL(pred_pair_offs_kernel, dim3((Q * NTp + 255) / 256), dim3(256), 0, st, I0,
+                           Q, D, r, offp);
+      else if (!tile_vphase)
+        hipLaunchKernelGGL(pred_offs_kernel, dim3((Q * D + 255) / 256), dim3(256), 0, st, I0, Q, D,
+                           r, offs);
+    }
     if (timing) (void)hipEventRecord(ev[1], st);
     dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
     if (pairs) {

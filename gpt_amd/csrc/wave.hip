@@ -963,10 +963,12 @@ hipError_t launch_wave(const StepParams& P, const ChainDesc* chains, int nchains
 // ------------------------------------------------------------------------ expm unit check (tests)
 namespace gpt {
 // One wave per matrix: wv_expm (mode 0) or the grid engine's wave_expm (mode 1) of an NN × NN
-// row-major matrix; NaN flags in bad.
+// row-major matrix; NaN flags in bad.  Mode 2 (timing, gpt_debug_expm_stamps): wv_expm as geod
+// calls it (three slots, the first NN/2 result columns) with s_memtime stamps per matrix in
+// st[4·m + 0..3]: entry, polynomial done, solve done, exit.
 template <int NN>
 __global__ __launch_bounds__(64) void wv_expm_check_kernel(const double* A, double* E, int32_t* bad,
-                                                           int mode) {
+                                                           int mode, long long* st) {
   extern __shared__ __attribute__((aligned(16))) double wv_sm[];
   const int lane = lane_id();
   const double* a = A + (size_t)blockIdx.x * NN * NN;
@@ -975,7 +977,13 @@ __global__ __launch_bounds__(64) void wv_expm_check_kernel(const double* A, doub
   wave_sync();
   bool b;
   const double* res;
-  if (mode == 0) {
+  long long* sm = st ? st + 4 * (size_t)blockIdx.x : nullptr;
+  if (sm && lane == 0) sm[0] = (long long)__builtin_amdgcn_s_memtime();
+  if (mode == 2) {
+    b = wv_expm<NN>(S0, S0 + NN * NN, S0 + 2 * NN * NN, lane, sm ? sm + 1 : nullptr, NN / 2);
+    if (sm && lane == 0) sm[3] = (long long)__builtin_amdgcn_s_memtime();
+    res = S0 + NN * NN;
+  } else if (mode == 0) {
     b = wv_expm<NN>(S0, S0 + NN * NN, S0 + 2 * NN * NN, lane);
     res = S0 + NN * NN;
   } else {
@@ -988,15 +996,15 @@ __global__ __launch_bounds__(64) void wv_expm_check_kernel(const double* A, doub
 }
 
 hipError_t launch_expm_check(int nn, int count, const double* A, double* E, int32_t* bad, int mode,
-                             hipStream_t st) {
+                             hipStream_t st, long long* stamps) {
 #define CASE(NNV)                                                                               \
   if (nn == NNV) {                                                                              \
-    const size_t lds = 8 * (size_t)7 * NNV * NNV;                                               \
+    const size_t lds = 8 * (size_t)(mode == 2 ? 3 : 7) * NNV * NNV;                             \
     hipError_t e = hipFuncSetAttribute((const void*)wv_expm_check_kernel<NNV>,                 \
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
     if (e != hipSuccess) return e;                                                              \
     hipLaunchKernelGGL(wv_expm_check_kernel<NNV>, dim3(count), dim3(64), lds, st, A, E, bad,    \
-                       mode);                                                                   \
+                       mode, stamps);                                                           \
     return hipGetLastError();                                                                   \
   }
   CASE(12) CASE(16) CASE(20) CASE(24) CASE(30) CASE(32) CASE(40)

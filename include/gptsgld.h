@@ -164,6 +164,10 @@ int64_t gpt_sgld_timeline_slots(void);
  * grid engine's wave_expm; bad[c] = 1 when E_c holds a NaN (the geodesic bail-out test). */
 int gpt_debug_expm(int32_t nn, int32_t count, int32_t mode, const double* A, double* E,
                    int32_t* bad);
+/* Timing of the wave engine's expm as geod calls it (three LDS slots, the first nn/2 result
+ * columns), one wave per matrix: stamps[4·m + 0..3] = s_memtime at entry, after the Padé
+ * polynomial, after the solve, at exit (diagnostics; scripts/expm_bench.py). */
+int gpt_debug_expm_stamps(int32_t nn, int32_t count, const double* A, int64_t* stamps);
 int gpt_sgld_session_timeline(gpt_sgld_session* s, int64_t nsteps, int64_t* out, double* event_us);
 /* Copy chain c's stores / status back (status: GPT_OK or GPT_ERR_NAN_GEODESIC; stores are
  * zero-filled for a non-zero status). */
