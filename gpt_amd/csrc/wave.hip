@@ -140,12 +140,13 @@ template <int NN>
 __device__ __forceinline__ bool wv_solve_dd_passes(const double* M, double* X, int lane, int ncols) {
   static_assert(NN > 32 && NN < 64, "one X column per lane beside M's");
   bool dd = true;
-  if (lane < NN) {
+  {
+    const int lc = min(lane, NN - 1);
     double off = 0.0;
-#pragma unroll 4
+#pragma unroll
     for (int i = 0; i < NN; ++i)
-      if (i != lane) off += fabs(M[i * NN + lane]);
-    dd = fabs(M[lane * NN + lane]) > off;
+      if (i != lc) off += fabs(M[i * NN + lc]);
+    dd = lane >= NN || fabs(M[lc * NN + lc]) > off;
   }
   if (!__all(dd)) return false;
 #pragma unroll 1
@@ -166,9 +167,11 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
                                         long long* st = nullptr, int ncols = NN) {
   constexpr int BS = Blk<NN>::BS;
   double cs = 0.0;
-  if (lane < NN) {
-#pragma unroll 4
-    for (int i = 0; i < NN; ++i) cs += fabs(S0[i * NN + lane]);
+  {
+    const int lc = min(lane, NN - 1);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) cs += fabs(S0[i * NN + lc]);
+    if (lane >= NN) cs = 0.0;
   }
   const double nA = wave_max(cs);
   int si = 0;
@@ -298,7 +301,11 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
     wave_sync();
   }
   bool bad = false;
-  for (int o = lane; o < NN * NN; o += 64) bad |= (o % NN < nc) && (S1[o] != S1[o]);
+#pragma unroll
+  for (int o0 = 0; o0 < NN * NN; o0 += 64) {            // every read in flight at once
+    const int o = o0 + lane;
+    if (o < NN * NN) bad |= (o % NN < nc) && (S1[o] != S1[o]);
+  }
   return __any(bad);
 }
 
@@ -425,12 +432,36 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
   // lanes = batch rows, waves = slices of the core entries
   const int i = lane, ic = min(lane, Bt - 1);
   {
+    // V[q, i] = Π_k temp[k, I[q,k], i] left to right (1.0 times the first factor is exact);
+    // four q per pass with their stores after all reads, so the reads of one pass are in flight
+    // together (a store in between would order every later read behind it)
+    auto vq = [&](int q) {
+      const unsigned short* to = toff_l + q * D;
+      double x = 1.0;
+      for (int k0 = 0; k0 < D; k0 += 8) {
+        double t8[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) t8[kk] = k0 + kk < D ? temp_l[to[k0 + kk] + ic] : 1.0;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) x *= t8[kk];
+      }
+      return x;
+    };
     const int Qw = (Q + 7) / 8, qa = wv * Qw, qb = min(Q, qa + Qw);
     double f = 0.0;
-    for (int q = qa; q < qb; ++q) {
-      const unsigned short* to = toff_l + q * D;
-      double v = temp_l[to[0] + ic];
-      for (int k = 1; k < D; ++k) v *= temp_l[to[k] + ic];
+    int q = qa;
+    for (; q + 4 <= qb; q += 4) {
+      double v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = vq(q + u);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (i < Bt) V_l[(q + u) * MV + i] = v[u];
+        f = fma(w_l[q + u], v[u], f);
+      }
+    }
+    for (; q < qb; ++q) {
+      const double v = vq(q);
       if (i < Bt) V_l[q * MV + i] = v;
       f = fma(w_l[q], v, f);
     }
