@@ -1598,6 +1598,8 @@ struct CfFold {
 // epoch / eval launch, read after the per-epoch status copy that synchronises anyway.
 struct CfTiming { double epoch_ms, eval_ms; int64_t epochs, evals, fold_steps; };
 static thread_local CfTiming g_cf_timing{};
+// GPTSGLD_CF_STAMPS=1: per-phase s_memtime of fold 0's first epoch (gpt_cf_last_stamps)
+static thread_local std::vector<long long> g_cf_stamps;
 
 static int cf_sgd_run(
     const char* name, std::vector<CfFold>& folds, const double* UserData, int64_t n1, int64_t D1,
@@ -1614,7 +1616,7 @@ static int cf_sgd_run(
          f.testpred_store && f.trainRMSE && f.testRMSE && f.N >= 1 && f.Ntest >= 1 &&
          f.ldr >= f.N && f.ldt >= f.Ntest && f.N == folds[0].N;
   if (!ok) { set_error(std::string("bad ") + name + " arguments"); return GPT_ERR_BAD_DIMS; }
-  if (!cf_rank_supported((int)r) || cf_lds_bytes((int)r, (int)m) > 160 * 1024) {
+  if (!cf_rank_supported((int)r) || cf_lds_bytes((int)r, (int)m, (int)(D1 + D2)) > 160 * 1024) {
     set_error(std::string(name) + ": rank not instantiated (1-6,8,10,12,15,16,20) or minibatch too large");
     return GPT_ERR_BAD_DIMS;
   }
@@ -1707,6 +1709,14 @@ static int cf_sgd_run(
   P.epsw = epsw; P.epsU = epsU; P.langevin = langevin; P.stiefel = stiefel; P.seed = seed;
   P.fixw = fixw ? 1 : 0;
   P.uptr = d_up.as<int32_t>(); P.ufe = d_uf.as<int32_t>(); P.vptr = d_vp.as<int32_t>(); P.vfe = d_vf.as<int32_t>();
+  DevMem d_stamps;
+  const bool want_stamps = std::getenv("GPTSGLD_CF_STAMPS") != nullptr;
+  g_cf_stamps.clear();
+  if (want_stamps) {
+    HIPCHK(d_stamps.alloc(8 * (size_t)kCfStampSteps * kCfStampSlots));
+    HIPCHK(hipMemset(d_stamps.p, 0, 8 * (size_t)kCfStampSteps * kCfStampSlots));
+    P.stamps = d_stamps.as<long long>();
+  }
   for (CfFold& fd : folds) {
     if (fd.w_store) std::memset(fd.w_store, 0, 8 * rr * maxepoch);
     std::memset(fd.U_store, 0, 8 * nU * maxepoch);
@@ -1732,10 +1742,27 @@ static int cf_sgd_run(
     host_randperm((int)N, seed, (int)(epoch - 1), perm.data());
     HIPCHK(hipMemcpy(d_perm.p, perm.data(), 4 * N, hipMemcpyHostToDevice));
     HIPCHK(hipEventRecord(evs.e[0], nullptr));
-    hipError_t e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, (epoch - 1) * nbatch, nbatch, nullptr);
+    hipError_t e = hipSuccess;
+    if (stiefel) {
+      // the Stiefel move needs Grams over every row: the whole epoch in one workgroup per fold
+      e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, (epoch - 1) * nbatch, 0, nbatch, 1, nullptr);
+    } else {
+      // per minibatch: the batch phase (one workgroup per fold), then the row-parallel move of U
+      // and V over the whole GPU (cf_move_kernel)
+      for (int b = 0; b < nbatch && e == hipSuccess; ++b) {
+        const long long step = (epoch - 1) * nbatch + b;
+        e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, step, b, 1, 0, nullptr);
+        if (e == hipSuccess) e = launch_cf_move(P, d_ch.as<CfChain>(), F, step, nullptr);
+      }
+    }
     if (e != hipSuccess) return hip_fail(e, "cf epoch kernel");
     HIPCHK(hipEventRecord(evs.e[1], nullptr));
     HIPCHK(hipEventSynchronize(evs.e[1]));
+    if (P.stamps) {                // the first epoch only
+      g_cf_stamps.resize((size_t)kCfStampSteps * kCfStampSlots);
+      HIPCHK(hipMemcpy(g_cf_stamps.data(), P.stamps, 8 * g_cf_stamps.size(), hipMemcpyDeviceToHost));
+      P.stamps = nullptr;
+    }
     {
       float ms = 0.f;
       HIPCHK(hipEventElapsedTime(&ms, evs.e[0], evs.e[1]));
@@ -1874,6 +1901,13 @@ extern "C" int gpt_cf_last_timing(double* epoch_ms, double* eval_ms, int64_t* ep
   *epochs = g_cf_timing.epochs;
   *fold_steps = g_cf_timing.fold_steps;
   return GPT_OK;
+}
+
+extern "C" int64_t gpt_cf_last_stamps(int64_t* out, int64_t cap) {
+  const int64_t n = (int64_t)g_cf_stamps.size();
+  if (out)
+    for (int64_t i = 0; i < std::min(n, cap); ++i) out[i] = g_cf_stamps[(size_t)i];
+  return n;
 }
 
 extern "C" int gpt_cf_fixw_sideinfo(

@@ -18,6 +18,14 @@ namespace gpt {
 constexpr int kCfNT = 1024;
 constexpr int kCfNW = kCfNT / 64;
 
+// Diagnostic phase stamps of the epoch kernel (P.stamps, gpt_cf_last_stamps): thread 0 of chain 0
+// records s_memtime after the barrier closing each phase of the first kCfStampSteps steps.
+#define CF_STAMP(bt, slot)                                                                   \
+  do {                                                                                       \
+    if (P.stamps && blockIdx.x == 0 && threadIdx.x == 0 && (bt) < kCfStampSteps)            \
+      P.stamps[(size_t)(bt) * kCfStampSlots + (slot)] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+
 // Sum of A[:, a]·B[:, b] over `rows` for every (a, b) < r², one wave per entry (wave sums).
 __device__ void cf_gram(const double* A, const double* B, int rows, int r, double* out) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -184,9 +192,70 @@ __device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int w
   return true;
 }
 
+// The SGD / SGLD move of U and V without the Stiefel geometry (the update block of :481-507 with
+// stiefel = false) touches every row independently, so it runs outside the epoch kernel's single
+// workgroup: grid (blocks, folds), one (row, column pair) per thread, the same doubles and noise
+// indices as cf_move.  G rows are zeroed for the next batch.
+// With at most 8 folds the grid is XCD-aware: workgroup x runs on XCD x mod 8 (round-robin
+// dispatch), so fold f's rows are moved by workgroups of XCD f — the XCD of the fold's epoch
+// workgroup (blockIdx.x = f), whose next batch then reads U and V from its own L2.
+template <int R>
+__global__ __launch_bounds__(256) void cf_move_kernel(CfParams P, const CfChain* chains,
+                                                      long long step, int nchains) {
+  int fold, blk;
+  if (nchains <= 8) {
+    fold = blockIdx.x & 7;
+    blk = blockIdx.x >> 3;
+    if (fold >= nchains) return;
+  } else {
+    fold = blockIdx.y;
+    blk = blockIdx.x;
+  }
+  const CfChain C = chains[fold];
+  if (__hip_atomic_load(C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  constexpr int RE = R + (R & 1);
+  const int nU = P.rowsU * (RE / 2);
+  const int o0 = blk * 256 + threadIdx.x;
+  if (o0 >= nU + P.rowsV * (RE / 2)) return;
+  const int which = o0 >= nU ? 1 : 0;
+  const int o = o0 - which * nU;
+  const int rows = which ? P.rowsV : P.rowsU;
+  double* M = which ? C.V : C.U;
+  double* G = which ? C.GV : C.GU;
+  const int lp = o / rows, row = o - lp * rows;
+  const double su2 = P.sigma_u * P.sigma_u;
+  double z[2] = {0.0, 0.0};
+  if (P.langevin)
+    normal_pair(P.seed, (uint32_t)((2 * lp + RE * row) >> 1), (uint32_t)step, kCfUVNoise,
+                (uint32_t)which, z[0], z[1]);
+  const double sq = sqrt(P.epsU);
+  double m0[2], g0[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int l = min(2 * lp + h, R - 1);
+    m0[h] = gptr(M)[row + (size_t)rows * l];
+    g0[h] = gptr(G)[row + (size_t)rows * l];
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int l = 2 * lp + h;
+    if (l >= R) break;
+    const size_t e = row + (size_t)rows * l;
+    double mn = m0[h] + P.epsU * (g0[h] - m0[h] / su2) / 2;
+    if (P.langevin) mn = mn + sq * z[h];
+    gptr_w(M)[e] = mn;
+    gptr_w(G)[e] = 0.0;
+  }
+}
+
+// domove = 0: only the batch phase of each step (sums, residuals, gradw + the w step, the
+// gradient rows); the caller launches cf_move_kernel between steps.  bt0: the launch's first
+// batch of the epoch, step0 its step.
 template <int R>
 __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfChain* chains,
-                                                         long long step0, int nb) {
+                                                         long long step0, int bt0, int nb,
+                                                         int domove) {
+
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const CfChain C = chains[blockIdx.x];
   const int tid = threadIdx.x, m = P.m, N = C.N;
@@ -208,14 +277,19 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
   int* unx = ms + m;                            // m
   int* vnx = unx + m;                           // m
   const bool masks = P.D1 <= 64 && P.D2 <= 64;
+  // with the masks: per feature row (users' D1, then movies' D2) the batch positions carrying it,
+  // ascending (fcnt of them), so its gradient sums only those ratings
+  int* fcnt = vnx + m;                          // D1 + D2
+  unsigned short* flist = (unsigned short*)(fcnt + P.D1 + P.D2);   // (D1 + D2) × m
   // Stiefel scratch of the U / V moves: aliases the batch buffers (sU .. ms), which are dead from
   // the barrier before the moves until the next batch reloads them (r = 20 fits 160 KB this way)
   double* scr = sU;
   if (__hip_atomic_load(C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   for (int o = tid; o < R * R; o += kCfNT) w_l[o] = C.w[o];
   const double is2 = 1.0 / P.signal_var;
-  for (int bt = 0; bt < nb; ++bt) {
-    const long long step = step0 + bt;
+  for (int bt = bt0; bt < bt0 + nb; ++bt) {
+    CF_STAMP(bt, 0);
+    const long long step = step0 + (bt - bt0);
     const int B = min(m, N - bt * m);
     const double cN = (double)N / (double)B;
     for (int ii = tid; ii < B; ii += kCfNT) {
@@ -225,6 +299,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       er[ii] = C.tr_rating[idx];
     }
     __syncthreads();
+    CF_STAMP(bt, 1);
     // per (side, ii): the feature bitmask, the first-occurrence flag and the next occurrence
     for (int o = tid; o < 2 * B; o += kCfNT) {
       const int side = o >= B ? 1 : 0, ii = o - side * B;
@@ -240,14 +315,22 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       }
       bool first = true;
       int nx = -1;
-      for (int z = 0; z < B; ++z) {
-        const bool same = ids[z] == id;
-        first &= !(same && z < ii);
-        if (same && z > ii && nx < 0) nx = z;
+      for (int z0 = 0; z0 < B; z0 += 8) {              // eight ids read before they are compared
+        int iz[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) iz[u] = z0 + u < B ? ids[z0 + u] : -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int z = z0 + u;
+          const bool same = iz[u] == id;
+          first &= !(same && z < ii);
+          if (same && z > ii && nx < 0) nx = z;
+        }
       }
       (side ? vnx : unx)[ii] = (nx + 1) | (first ? 1 << 16 : 0);
     }
     __syncthreads();
+    CF_STAMP(bt, 2);
     // sumU = U[user,:] + b·sum(U[uidx,:],1), sumV likewise (:462); the feature rows in ascending
     // order (find(UserData[i,:]), the CSR order)
     for (int o = tid; o < 2 * B * R; o += kCfNT) {
@@ -272,7 +355,24 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       const double v = gptr(M)[id + (size_t)rows * l] + (side ? P.c : P.b) * f;
       (side ? sV : sU)[ii * R + l] = v;
     }
+    if (masks)
+      for (int o = tid; o < P.D1 + P.D2; o += kCfNT) {
+        const int side = o >= P.D1 ? 1 : 0, f = o - side * P.D1;
+        const uint64_t* mk = side ? vmk : umk;
+        unsigned short* lst = flist + (size_t)o * m;
+        int c = 0;
+        for (int z0 = 0; z0 < B; z0 += 8) {
+          uint64_t m8[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) m8[u] = z0 + u < B ? mk[z0 + u] : 0ull;
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if ((m8[u] >> f) & 1ull) lst[c++] = (unsigned short)(z0 + u);
+        }
+        fcnt[o] = c;
+      }
     __syncthreads();
+    CF_STAMP(bt, 3);
     for (int o = tid; o < B * R; o += kCfNT) {
       const int ii = o / R, j = o - ii * R;
       double s1 = 0.0, s2 = 0.0;
@@ -285,6 +385,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       tV[ii * R + j] = s2;
     }
     __syncthreads();
+    CF_STAMP(bt, 4);
     for (int ii = tid; ii < B; ii += kCfNT) {       // residual rating − a·sum((sumU*w).*sumV)
       double s = 0.0;
 #pragma unroll
@@ -292,13 +393,22 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       er[ii] = er[ii] - P.a * s;
     }
     __syncthreads();
+    CF_STAMP(bt, 5);
     // gradw (:466, :473-477) and the w step of :479-483 into wn
     // (GPT_fixw / GPT_fixw_sideinfo, :56-156 / :282-404: w is fixed — no gradw, no step)
     for (int o = tid; o < R * R; o += kCfNT) {
       if (P.fixw) { wn_l[o] = w_l[o]; continue; }
       const int i = o % R, j = o / R;
       double g = 0.0;
-      for (int ii = 0; ii < B; ++ii) g += er[ii] * (sU[ii * R + i] * sV[ii * R + j]) * is2;
+      int ii = 0;
+      for (; ii + 4 <= B; ii += 4) {                   // four ratings' reads in flight, summed in order
+        double t4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t4[u] = er[ii + u] * (sU[(ii + u) * R + i] * sV[(ii + u) * R + j]) * is2;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g += t4[u];
+      }
+      for (; ii < B; ++ii) g += er[ii] * (sU[ii * R + i] * sV[ii * R + j]) * is2;
       const double G = g * cN - w_l[o] / (P.sigma_w * P.sigma_w);
       double wn = w_l[o] + P.epsw * G / 2;
       if (P.langevin)
@@ -329,9 +439,14 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       double g = 0.0;
       bool hit = false;
       if (masks) {
-        const uint64_t* mk = side ? vmk : umk;
-        for (int z = 0; z < B; ++z)
-          if ((mk[z] >> f) & 1ull) { g += ab * (er[z] * T[z * R + l]) * is2; hit = true; }
+        const int fo = side ? P.D1 + f : f;
+        const unsigned short* lst = flist + (size_t)fo * m;
+        const int c = fcnt[fo];
+        hit = c > 0;
+        for (int x = 0; x < c; ++x) {
+          const int z = lst[x];
+          g += ab * (er[z] * T[z * R + l]) * is2;
+        }
       } else {
         const int32_t* ptr = side ? P.vptr : P.uptr;
         const int32_t* fe = side ? P.vfe : P.ufe;
@@ -345,11 +460,13 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       if (hit) gptr_w(side ? C.GV : C.GU)[row + (size_t)(side ? P.rowsV : P.rowsU) * l] = g * cN;
     }
     __syncthreads();
-    if (!cf_move<R>(P, C.U, C.GU, P.rowsU, 0, step, scr) ||
-        !cf_move<R>(P, C.V, C.GV, P.rowsV, 1, step, scr)) {
+    CF_STAMP(bt, 6);
+    if (domove && (!cf_move<R>(P, C.U, C.GU, P.rowsU, 0, step, scr) ||
+                   !cf_move<R>(P, C.V, C.GV, P.rowsV, 1, step, scr))) {
       if (tid == 0) __hip_atomic_store(C.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
+    CF_STAMP(bt, 7);
     for (int o = tid; o < R * R; o += kCfNT) w_l[o] = wn_l[o];
     __syncthreads();
   }
@@ -551,9 +668,9 @@ hipError_t launch_cfg_kron(int r, const double* U, int n1, const double* V, int 
   return hipGetLastError();
 }
 
-size_t cf_lds_bytes(int r, int m) {
+size_t cf_lds_bytes(int r, int m, int nfeat) {
   const size_t base = 8 * (2 * (size_t)r * r + 4 * (size_t)m * r + m) + 16 * (size_t)m +
-                      4 * (4 * (size_t)m + 2);
+                      4 * (4 * (size_t)m + 2) + 4 * (size_t)nfeat + 2 * (size_t)nfeat * m + 16;
   const size_t nn = 2 * (size_t)r;
   const size_t stf = 8 * (3 * (size_t)r * r + 7 * nn * nn + 7 * (size_t)r * r + nn * r + r) + 16;
   const size_t moves = 8 * 2 * (size_t)r * r + stf;      // w | wn | Stiefel scratch over the batch
@@ -572,17 +689,34 @@ bool cf_rank_supported(int r) {
 }
 
 hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
-                           int nb, hipStream_t st) {
-  const size_t lds = cf_lds_bytes(P.r, P.m);
+                           int bt0, int nb, int domove, hipStream_t st) {
+  const size_t lds = cf_lds_bytes(P.r, P.m, P.D1 + P.D2);
   switch (P.r) {
 #define CASE(RR)                                                                              \
   case RR: {                                                                                  \
-    static std::atomic<uint64_t> attr{0};                                                         \
-    hipError_t e = set_max_lds_once((const void*)cf_epoch_kernel<RR>, 160 * 1024, attr);          \
-    if (e != hipSuccess) return e;                                                                \
+    static std::atomic<uint64_t> attr{0};                                                     \
+    hipError_t e = set_max_lds_once((const void*)cf_epoch_kernel<RR>, 160 * 1024, attr);      \
+    if (e != hipSuccess) return e;                                                            \
     hipLaunchKernelGGL(cf_epoch_kernel<RR>, dim3(nchains), dim3(kCfNT), lds, st, P, chains,   \
-                       step0, nb);                                                            \
+                       step0, bt0, nb, domove);                                               \
   } break;
+    GPT_CF_RANKS(CASE)
+#undef CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_cf_move(const CfParams& P, const CfChain* chains, int nchains, long long step,
+                          hipStream_t st) {
+  const int RE = P.r + (P.r & 1);
+  const unsigned blocks = (unsigned)(((long long)(P.rowsU + P.rowsV) * (RE / 2) + 255) / 256);
+  const dim3 grid = nchains <= 8 ? dim3(8 * blocks) : dim3(blocks, nchains);
+  switch (P.r) {
+#define CASE(RR)                                                                              \
+  case RR:                                                                                    \
+    hipLaunchKernelGGL(cf_move_kernel<RR>, grid, dim3(256), 0, st, P, chains, step, nchains);  \
+    break;
     GPT_CF_RANKS(CASE)
 #undef CASE
     default: return hipErrorInvalidValue;

@@ -237,7 +237,9 @@ struct CfParams {
   const int32_t* ufe;
   const int32_t* vptr;   // n2+1
   const int32_t* vfe;
+  long long* stamps;     // diagnostics: kCfStampSteps x kCfStampSlots s_memtime of chain 0, or null
 };
+constexpr int kCfStampSteps = 64, kCfStampSlots = 8;
 
 struct CfChain {
   const int32_t* tr_user;   // N   0-based ids
@@ -260,10 +262,12 @@ struct CfChain {
   int32_t* status;
 };
 
-size_t cf_lds_bytes(int r, int m);
+size_t cf_lds_bytes(int r, int m, int nfeat);
 bool cf_rank_supported(int r);
 hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
-                           int nb, hipStream_t st);
+                           int bt0, int nb, int domove, hipStream_t st);
+hipError_t launch_cf_move(const CfParams& P, const CfChain* chains, int nchains, long long step,
+                          hipStream_t st);
 hipError_t launch_cf_eval(const CfParams& P, const CfChain* chains, int nchains, int nmax,
                           int counter, hipStream_t st);
 hipError_t launch_cfg_rows(int side, int r, const double* W, const double* Oth, int rows_oth,

@@ -314,6 +314,11 @@ int gpt_cf_fullw_sideinfo_folds(int64_t F, const double* const* Rating, const in
  * launches, fold_steps = minibatch steps summed over the folds live in each launch.  No
  * reference counterpart (measurement, bench.py --workload movielens). */
 int gpt_cf_last_timing(double* epoch_ms, double* eval_ms, int64_t* epochs, int64_t* fold_steps);
+/* With GPTSGLD_CF_STAMPS set, the last CF SGD call recorded s_memtime at the 8 phase boundaries
+ * of fold 0's first 64 steps of its first epoch (batch load, masks / links, sums, sum·w,
+ * residuals, gradients, U / V moves): copies up to cap of them (64 x 8, step-major) and returns
+ * how many there are (0 without the variable).  Diagnostics. */
+int64_t gpt_cf_last_stamps(int64_t* out, int64_t cap);
 
 /* The other SGD / SGLD variants of the CF model (same Rating / Ratingtest / output conventions
  * as gpt_cf_fullw_sideinfo; the NaN bail-out zeroes the parameter stores):
