@@ -1671,9 +1671,9 @@ static int cf_sgd_run(
       if (eu[i] < 0 || eu[i] >= n1 || em[i] < 0 || em[i] >= n2) { set_error("test rating ids out of range"); return GPT_ERR_BAD_DIMS; }
     }
     // one allocation per fold: ids (int32) first, then doubles (8-B aligned offsets)
-    const size_t ints = (size_t)(2 * N + 2 * Nt + 2);
+    const size_t ints = (size_t)(4 * N + 2 * Nt + 2);
     const size_t dbl0 = (ints * 4 + 15) / 16 * 2;                     // in doubles
-    const size_t ndbl = (size_t)N + Nt + rr + 2 * nU + 2 * nV + N + Nt + 2 * (size_t)neval;
+    const size_t ndbl = (size_t)N + Nt + rr + 2 * nU + 2 * nV + N + Nt + 2 * (size_t)neval + N;
     std::unique_ptr<DevMem> dm(new DevMem());
     HIPCHK(dm->alloc(8 * (dbl0 + ndbl)));
     int32_t* ip = dm->as<int32_t>();
@@ -1684,6 +1684,8 @@ static int cf_sgd_run(
     C.tr_rating = dp; C.te_rating = dp + N;
     C.w = dp + N + Nt; C.U = C.w + rr; C.V = C.U + nU; C.GU = C.V + nV; C.GV = C.GU + nU;
     C.trainpred = C.GV + nV; C.testpred = C.trainpred + N; C.sse = C.testpred + Nt;
+    C.ep_user = ip + 2 * N + 2 * Nt + 2; C.ep_movie = C.ep_user + N;
+    C.ep_rating = C.sse + 2 * (size_t)neval;
     C.N = (int)N; C.Ntest = (int)Nt; C.perm = d_perm.as<int32_t>();
     C.status = d_st[f]; C.ymean = fd.ymean; C.ystd = fd.ystd;
     d_w[f] = C.w; d_U[f] = C.U; d_V[f] = C.V; d_sse[f] = C.sse; d_tep[f] = C.testpred;
@@ -1709,6 +1711,18 @@ static int cf_sgd_run(
   P.epsw = epsw; P.epsU = epsU; P.langevin = langevin; P.stiefel = stiefel; P.seed = seed;
   P.fixw = fixw ? 1 : 0;
   P.uptr = d_up.as<int32_t>(); P.ufe = d_uf.as<int32_t>(); P.vptr = d_vp.as<int32_t>(); P.vfe = d_vf.as<int32_t>();
+  DevMem d_masks;
+  if (D1 <= 64 && D2 <= 64) {    // each user's / movie's feature rows as one 64-bit mask
+    std::vector<uint64_t> mk((size_t)(n1 + n2), 0);
+    for (int64_t i = 0; i < n1; ++i)
+      for (int z = uptr[i]; z < uptr[i + 1]; ++z) mk[i] |= 1ull << (ufe[z] - n1);
+    for (int64_t i = 0; i < n2; ++i)
+      for (int z = vptr[i]; z < vptr[i + 1]; ++z) mk[n1 + i] |= 1ull << (vfe[z] - n2);
+    HIPCHK(d_masks.alloc(8 * mk.size()));
+    HIPCHK(hipMemcpy(d_masks.p, mk.data(), 8 * mk.size(), hipMemcpyHostToDevice));
+    P.umask = d_masks.as<uint64_t>();
+    P.vmask = P.umask + n1;
+  }
   DevMem d_stamps;
   const bool want_stamps = std::getenv("GPTSGLD_CF_STAMPS") != nullptr;
   g_cf_stamps.clear();
@@ -1742,6 +1756,10 @@ static int cf_sgd_run(
     host_randperm((int)N, seed, (int)(epoch - 1), perm.data());
     HIPCHK(hipMemcpy(d_perm.p, perm.data(), 4 * N, hipMemcpyHostToDevice));
     HIPCHK(hipEventRecord(evs.e[0], nullptr));
+    {
+      const hipError_t eg = launch_cf_gather(d_ch.as<CfChain>(), F, (int)N, nullptr);
+      if (eg != hipSuccess) return hip_fail(eg, "cf gather kernel");
+    }
     hipError_t e = hipSuccess;
     if (stiefel) {
       // the Stiefel move needs Grams over every row: the whole epoch in one workgroup per fold

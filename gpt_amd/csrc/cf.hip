@@ -293,10 +293,9 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     const int B = min(m, N - bt * m);
     const double cN = (double)N / (double)B;
     for (int ii = tid; ii < B; ii += kCfNT) {
-      const int idx = C.perm[bt * m + ii];
-      us[ii] = C.tr_user[idx];
-      ms[ii] = C.tr_movie[idx];
-      er[ii] = C.tr_rating[idx];
+      us[ii] = C.ep_user[bt * m + ii];                // the epoch's order (cf_gather_kernel)
+      ms[ii] = C.ep_movie[bt * m + ii];
+      er[ii] = C.ep_rating[bt * m + ii];
     }
     __syncthreads();
     CF_STAMP(bt, 1);
@@ -305,14 +304,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       const int side = o >= B ? 1 : 0, ii = o - side * B;
       const int* ids = side ? ms : us;
       const int id = ids[ii];
-      if (masks) {
-        const int32_t* ptr = side ? P.vptr : P.uptr;
-        const int32_t* fe = side ? P.vfe : P.ufe;
-        const int base = side ? P.n2 : P.n1;
-        uint64_t mk = 0;
-        for (int z = ptr[id]; z < ptr[id + 1]; ++z) mk |= 1ull << (fe[z] - base);
-        (side ? vmk : umk)[ii] = mk;
-      }
+      if (masks) (side ? vmk : umk)[ii] = (side ? P.vmask : P.umask)[id];
       bool first = true;
       int nx = -1;
       for (int z0 = 0; z0 < B; z0 += 8) {              // eight ids read before they are compared
@@ -340,8 +332,21 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       const int id = side ? ms[ii] : us[ii];
       double f = 0.0;
       if (masks) {
+        // the first four feature rows' loads issued together, then summed in ascending order
         const int base = side ? P.n2 : P.n1;
         uint64_t mk = (side ? vmk : umk)[ii];
+        double fv[4];
+        bool fh[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          fh[u] = mk != 0;
+          const int fb = fh[u] ? __ffsll((long long)mk) - 1 : 0;
+          fv[u] = fh[u] ? gptr(M)[base + fb + (size_t)rows * l] : 0.0;
+          mk &= mk - 1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (fh[u]) f += fv[u];
         while (mk) {
           const int fb = __ffsll((long long)mk) - 1;
           mk &= mk - 1;
@@ -704,6 +709,24 @@ hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains
 #undef CASE
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// The training ratings of every fold in this epoch's order, once per epoch (the batch kernels
+// then read their minibatch contiguously instead of through the permutation).
+__global__ __launch_bounds__(256) void cf_gather_kernel(const CfChain* chains, int N) {
+  const CfChain C = chains[blockIdx.y];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N) return;
+  const int idx = C.perm[i];
+  C.ep_user[i] = C.tr_user[idx];
+  C.ep_movie[i] = C.tr_movie[idx];
+  C.ep_rating[i] = C.tr_rating[idx];
+}
+
+hipError_t launch_cf_gather(const CfChain* chains, int nchains, int N, hipStream_t st) {
+  hipLaunchKernelGGL(cf_gather_kernel, dim3((unsigned)((N + 255) / 256), nchains), dim3(256), 0,
+                     st, chains, N);
   return hipGetLastError();
 }
 

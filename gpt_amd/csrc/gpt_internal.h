@@ -237,6 +237,8 @@ struct CfParams {
   const int32_t* ufe;
   const int32_t* vptr;   // n2+1
   const int32_t* vfe;
+  const uint64_t* umask;   // n1: bitmask of each user's feature rows (D1 <= 64), else null
+  const uint64_t* vmask;   // n2
   long long* stamps;     // diagnostics: kCfStampSteps x kCfStampSlots s_memtime of chain 0, or null
 };
 constexpr int kCfStampSteps = 64, kCfStampSlots = 8;
@@ -250,6 +252,9 @@ struct CfChain {
   const double* te_rating;
   int N, Ntest;
   const int32_t* perm;      // N   this epoch's permutation (0-based rows of the ratings)
+  int32_t* ep_user;         // N   the training ratings in this epoch's order (cf_gather_kernel)
+  int32_t* ep_movie;
+  double* ep_rating;
   double* w;                // r*r column-major
   double* U;                // rowsU*r column-major
   double* V;                // rowsV*r
@@ -266,6 +271,7 @@ size_t cf_lds_bytes(int r, int m, int nfeat);
 bool cf_rank_supported(int r);
 hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
                            int bt0, int nb, int domove, hipStream_t st);
+hipError_t launch_cf_gather(const CfChain* chains, int nchains, int N, hipStream_t st);
 hipError_t launch_cf_move(const CfParams& P, const CfChain* chains, int nchains, long long step,
                           hipStream_t st);
 hipError_t launch_cf_eval(const CfParams& P, const CfChain* chains, int nchains, int nmax,
