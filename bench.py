@@ -349,7 +349,7 @@ def movielens_main(args):
     (the script runs r = 15; --r).  The folds run as sibling chains of one cf_epoch_kernel launch
     per epoch (gpt_cf_fullw_sideinfo_folds); value = minibatch steps summed over the folds / wall
     time of the whole call (host evaluation, stores and early stop included); roofline from the
-    device time of the epoch launches (hipEvents inside the library, gpt_cf_last_timing).  N > 1:
+    device time of each epoch's launches (hipEvents inside the library, gpt_cf_last_timing).  N > 1:
     every rank runs the experiment with its own param_seed (replicas, no collective)."""
     import torch
     import torch.distributed as dist
@@ -419,9 +419,12 @@ def movielens_main(args):
                        "parallelism": "folds%dx%d" % (len(folds), world)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "cf_epoch_kernel<%d>" % r,
-                         "kernel_us": ep_us, "kernel_us_note": "per epoch launch (every live fold's "
-                         "%d minibatch steps), hipEvents inside gpt_cf_fullw_sideinfo_folds" % nb,
+                         "kernel": "cf_gather_kernel + %d x (cf_epoch_kernel<%d> batch phase + "
+                                   "cf_move_kernel<%d>)" % (nb, r, r),
+                         "kernel_us": ep_us, "kernel_us_note": "per epoch of every live fold's %d "
+                         "minibatch steps (one batch-phase launch, one workgroup per fold, and one "
+                         "row-parallel move launch per step), hipEvents inside "
+                         "gpt_cf_fullw_sideinfo_folds around the epoch's launches" % nb,
                          "eval_kernel_us": 1e3 * tm["eval_ms"] / max(tm["epochs"], 1),
                          "algorithmic_bytes_per_step": bstep,
                          "algorithmic_bytes_per_launch": bstep * steps_per_launch,
