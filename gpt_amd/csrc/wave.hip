@@ -628,6 +628,8 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
   // ---- stage U^(k) (column-major, stride n) and coef_k (row i: R values) in LDS
   double* U_l = wv_sm;
   double* cf_l = U_l + n * R;
+  double* sctab = wv_sm + wv_dim_lds_dbl(n, R, m);
+  sincos_tab_fill(sctab, lane, 64);
   copy_to_lds<8>(U_l, Ug, n * R, lane, 64);
   copy_to_lds<8>(cf_l, Cp->coef + (size_t)k * m * R, Bt * R, lane, 64);
   wave_sync();
@@ -682,8 +684,8 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
 #pragma unroll
       for (int q = 0; q < NQJ; ++q) {
         double z[4];
-        normal_quad<4>(seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
-                       (uint32_t)k, z);
+        normal_quad_tab<4>(seed, (uint32_t)((l * NQ + q) * 64 + lane), (uint32_t)t, kUNoise,
+                           (uint32_t)k, sctab, z);
 #pragma unroll
         for (int L = 0; L < R; ++L) {
           if (l == L) {
@@ -748,19 +750,31 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
 #pragma unroll
     for (int b2 = 0; b2 < R; ++b2) g[jj][b2] = g[jj][b2] - s[b2] / 2;
   }
-#pragma unroll                     // static a: g stays in registers (g[jj][a] with a runtime a
-  for (int a = 0; a < R; ++a) {      // put the whole drive in scratch memory)
-    double v[R];
+  // S[a][b] for b >= a, rows a and R−1−a in one exact-count butterfly of R + 1 values (static a:
+  // g stays in registers — g[jj][a] with a runtime a put the whole drive in scratch memory)
 #pragma unroll
-    for (int b2 = 0; b2 < R; ++b2) {
+  for (int p = 0; p < (R + 1) / 2; ++p) {
+    const int a1 = p, a2 = R - 1 - p, n1 = R - a1;
+    const bool two = a2 > a1;
+    double v[R + 1];
+#pragma unroll
+    for (int x = 0; x < R + 1; ++x) {
+      const int a = x < n1 ? a1 : a2, b2 = x < n1 ? a1 + x : a2 + (x - n1);
       double s1 = 0.0;
-      if (b2 >= a) {
+      if (x < n1 || (two && b2 < R)) {
 #pragma unroll
         for (int jj = 0; jj < J; ++jj) s1 = fma(g[jj][a], g[jj][b2], s1);
       }
-      v[b2] = s1;
+      v[x] = s1;
     }
-    wv_sum_to_lds<R>(v, Sg + a * R, lane);               // S[a][b] valid for b >= a
+    obf_run<R + 1, R + 1>(v, lane);
+    int vi;
+    bool wr;
+    obf_index<R + 1>(lane, vi, wr);
+    if (wr) {
+      if (vi < n1) Sg[a1 * R + a1 + vi] = v[0];
+      else if (two && a2 + (vi - n1) < R) Sg[a2 * R + a2 + (vi - n1)] = v[0];
+    }
   }
   wave_sync();
   for (int o = lane; o < R * R; o += 64) {
@@ -917,7 +931,8 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
 
 static int wv_J(int n) { return n <= 64 ? 1 : (n <= 128 ? 2 : (n <= 192 ? 3 : (n <= 256 ? 4 : 0))); }
 
-size_t wv_dim_lds_bytes(int n, int r, int m) { return 8 * (size_t)wv_dim_lds_dbl(n, r, m); }
+// + the U noise's two 16-entry (sin, cos) tables (fm_sincos_tab2) past everything else
+size_t wv_dim_lds_bytes(int n, int r, int m) { return 8 * ((size_t)wv_dim_lds_dbl(n, r, m) + 64); }
 size_t wv_vphase_lds_bytes(int D, int r, int Q, int m) {
   return 8 * (size_t)wv_vphase_lds_dbl(D, r, Q, m);
 }
