@@ -90,12 +90,13 @@ def algorithmic_flops_per_step(n, D, B, r, Q):
 
 
 def executed_flops_per_step(n, D, B, r, Q):
-    """The flops the wave engine executes per step at the Padé degree the kin40k runs take (5: three
-    2r x 2r products, a 2r x 2r LU with 2r right-hand sides; the r x r expm likewise), for
-    comparison with the §8(d) count: phidotU + gradU 4nrDB, V / A 3QDB, fhat / gradw 4QB, proj +
-    Grams + tmpU D·(2nr² · 5 + 2·2nr·r), the expm D·(3·2(2r)³ + (8/3)(2r)³ + 3·2r³ + (8/3)r³)."""
+    """The flops the wave engine executes per step at the Padé degree the kin40k runs take (5 for
+    the 2r x 2r expm: three products, an LU and the r right-hand sides geod reads; degree 3 for the
+    r x r one: two products, an LU with r right-hand sides), for comparison with the §8(d) count:
+    phidotU + gradU 4nrDB, V / A 3QDB, fhat / gradw 4QB, proj + Grams + tmpU D·(2nr² · 5 + 2·2nr·r),
+    the expm D·(3·2(2r)³ + (2/3)(2r)³ + 2(2r)²·r + 2·2r³ + (8/3)r³)."""
     nn = 2 * r
-    expm = 3 * 2 * nn ** 3 + 8 * nn ** 3 / 3 + 3 * 2 * r ** 3 + 8 * r ** 3 / 3
+    expm = 3 * 2 * nn ** 3 + 2 * nn ** 3 / 3 + 2 * nn ** 2 * r + 2 * 2 * r ** 3 + 8 * r ** 3 / 3
     return (4 * n * r * D * B + 3 * Q * D * B + 4 * Q * B
             + D * (2 * n * r * r * 5 + 2 * 2 * n * r * r + expm))
 

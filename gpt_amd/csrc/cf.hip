@@ -324,41 +324,68 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     __syncthreads();
     CF_STAMP(bt, 2);
     // sumU = U[user,:] + b·sum(U[uidx,:],1), sumV likewise (:462); the feature rows in ascending
-    // order (find(UserData[i,:]), the CSR order)
-    for (int o = tid; o < 2 * B * R; o += kCfNT) {
-      const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
-      const double* M = side ? C.V : C.U;
-      const int rows = side ? P.rowsV : P.rowsU;
-      const int id = side ? ms[ii] : us[ii];
-      double f = 0.0;
-      if (masks) {
-        // the first four feature rows' loads issued together, then summed in ascending order
-        const int base = side ? P.n2 : P.n1;
-        uint64_t mk = (side ? vmk : umk)[ii];
-        double fv[4];
-        bool fh[4];
+    // order (find(UserData[i,:]), the CSR order).  With the masks: four (rating, column) items
+    // per thread and pass, every item's row loads issued before any sum (one memory latency per
+    // pass instead of one per item)
+    if (masks) {
+      for (int o0 = tid; o0 < 2 * B * R; o0 += 4 * kCfNT) {
+        double fv[4][4], mv[4];
+        bool fh[4][4], ok[4];
+        uint64_t rest[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          fh[u] = mk != 0;
-          const int fb = fh[u] ? __ffsll((long long)mk) - 1 : 0;
-          fv[u] = fh[u] ? gptr(M)[base + fb + (size_t)rows * l] : 0.0;
-          mk &= mk - 1;
+        for (int k4 = 0; k4 < 4; ++k4) {
+          const int o = o0 + k4 * kCfNT;
+          ok[k4] = o < 2 * B * R;
+          const int oc = ok[k4] ? o : o0;
+          const int side = oc / (B * R), x = oc - side * (B * R), ii = x / R, l = x - ii * R;
+          const double* M = side ? C.V : C.U;
+          const int rows = side ? P.rowsV : P.rowsU;
+          const int id = side ? ms[ii] : us[ii];
+          const int base = side ? P.n2 : P.n1;
+          uint64_t mk = (side ? vmk : umk)[ii];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            fh[k4][u] = mk != 0;
+            const int fb = fh[k4][u] ? __ffsll((long long)mk) - 1 : 0;
+            fv[k4][u] = fh[k4][u] ? gptr(M)[base + fb + (size_t)rows * l] : 0.0;
+            mk &= mk - 1;
+          }
+          rest[k4] = mk;
+          mv[k4] = gptr(M)[id + (size_t)rows * l];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (fh[u]) f += fv[u];
-        while (mk) {
-          const int fb = __ffsll((long long)mk) - 1;
-          mk &= mk - 1;
-          f += gptr(M)[base + fb + (size_t)rows * l];
+        for (int k4 = 0; k4 < 4; ++k4) {
+          if (!ok[k4]) continue;
+          const int o = o0 + k4 * kCfNT;
+          const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+          const double* M = side ? C.V : C.U;
+          const int rows = side ? P.rowsV : P.rowsU;
+          const int base = side ? P.n2 : P.n1;
+          double f = 0.0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (fh[k4][u]) f += fv[k4][u];
+          uint64_t mk = rest[k4];
+          while (mk) {
+            const int fb = __ffsll((long long)mk) - 1;
+            mk &= mk - 1;
+            f += gptr(M)[base + fb + (size_t)rows * l];
+          }
+          (side ? sV : sU)[ii * R + l] = mv[k4] + (side ? P.c : P.b) * f;
         }
-      } else {
+      }
+    } else {
+      for (int o = tid; o < 2 * B * R; o += kCfNT) {
+        const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+        const double* M = side ? C.V : C.U;
+        const int rows = side ? P.rowsV : P.rowsU;
+        const int id = side ? ms[ii] : us[ii];
         const int32_t* ptr = side ? P.vptr : P.uptr;
         const int32_t* fe = side ? P.vfe : P.ufe;
+        double f = 0.0;
         for (int z = ptr[id]; z < ptr[id + 1]; ++z) f += gptr(M)[fe[z] + (size_t)rows * l];
+        (side ? sV : sU)[ii * R + l] = gptr(M)[id + (size_t)rows * l] + (side ? P.c : P.b) * f;
       }
-      const double v = gptr(M)[id + (size_t)rows * l] + (side ? P.c : P.b) * f;
-      (side ? sV : sU)[ii * R + l] = v;
     }
     if (masks)
       for (int o = tid; o < P.D1 + P.D2; o += kCfNT) {

@@ -357,7 +357,8 @@ __device__ __forceinline__ void wv_map(int x, int nchains, int D, int& c, int& k
 // staged U^(k) (n·r) plus coef_k / the r × r Grams when those need more.
 GPT_HD int wv_dim_lds_dbl(int n, int r, int m) {
   const int slots = 12 * r * r;
-  const int pre = n * r + (m * r > 4 * r * r ? m * r : 4 * r * r);
+  const int mp = (m + 7) / 8 * 8;                       // coef_k rows padded to the gradU row ring
+  const int pre = n * r + (mp * r > 4 * r * r ? mp * r : 4 * r * r);
   return slots > pre ? slots : pre;
 }
 
@@ -632,6 +633,7 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
   sincos_tab_fill(sctab, lane, 64);
   copy_to_lds<8>(U_l, Ug, n * R, lane, 64);
   copy_to_lds<8>(cf_l, Cp->coef + (size_t)k * m * R, Bt * R, lane, 64);
+  for (int o = Bt * R + lane; o < (Bt + PF - 1) / PF * PF * R; o += 64) cf_l[o] = 0.0;
   wave_sync();
 
   // ---- gradU^(k) = (N/B)/σ² Σ_i φ[:,k,i]·coef[k][i][:]  (GPT_SGLD.jl:396-408)
@@ -657,14 +659,20 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
         const int inext = min(i0 + x + PF, Bt - 1);
 #pragma unroll
         for (int jj = 0; jj < J; ++jj) ring[x][jj] = rp.at(inext)[jc[jj]];
-        if (i0 + x < Bt) {
+        {
+          // no per-row branch (coef rows past Bt are zero: +0 added to each sum, exact), so the
+          // row ring's loads stay in flight across rows (a branch made the compiler wait for
+          // every outstanding load); the row's R coefficients are read together, waited for once
           const double* ci = cf_l + (i0 + x) * R;
+          double c[R];
 #pragma unroll
-          for (int l = 0; l < R; ++l) {
-            const double cv = ci[l];
+          for (int l = 0; l < R; ++l) c[l] = ci[l];
 #pragma unroll
-            for (int jj = 0; jj < J; ++jj) g[jj][l] = fma(p[jj], cv, g[jj][l]);
-          }
+          for (int l = 0; l < R; ++l) asm volatile("" : "+v"(c[l]));
+#pragma unroll
+          for (int l = 0; l < R; ++l)
+#pragma unroll
+            for (int jj = 0; jj < J; ++jj) g[jj][l] = fma(p[jj], c[l], g[jj][l]);
         }
       }
     }

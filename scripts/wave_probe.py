@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--n", type=int, default=150)
     ap.add_argument("--r", type=int, default=20)
+    ap.add_argument("--epsw", type=float, default=1e-4)
+    ap.add_argument("--epsU", type=float, default=1e-7)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     import torch
@@ -47,7 +49,7 @@ def main():
             if eng == "grid" and C > 64:
                 continue
             epochs = 2 + -(-(3 * args.steps) // nb)
-            s = SGLDSession(phi, y, I, r, Q, m, 1e-4, 1e-7, 0.0476, 0, epochs,
+            s = SGLDSession(phi, y, I, r, Q, m, args.epsw, args.epsU, 0.0476, 0, epochs,
                             list(range(1, C + 1)), store=False, engine=eng)
             s.run(50)
             s.prepare(args.steps)
