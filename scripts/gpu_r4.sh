@@ -33,7 +33,7 @@ for s in "$@"; do
     probe)  run probe 300 python -u scripts/wave_probe.py --chains 256,10 --engines wave --steps 200 --out gpurun_out/${T}_probe.json ;;
     quality) run quality 900 $PYT tests/test_gpu_quality.py tests/test_gpu_fullsize.py -k "not movielens" ;;
     ref)    run ref 600 python -u bench.py --workload kin40k_ref ;;
-    refprof) run refprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_ref -o ref -- python -u bench.py --workload kin40k_ref --no-cpu-baseline ;;
+    refprof) run refprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_ref -o ref -- python -u bench.py --workload kin40k_ref --no-cpu-baseline --epochs 20 ;;
     mlprof) run mlprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_ml -o ml -- python -u bench.py --workload movielens --no-cpu-baseline --epochs 40 ;;
     *) echo "unknown step $s" ;;
   esac
