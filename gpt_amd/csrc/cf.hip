@@ -475,7 +475,18 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         const unsigned short* lst = flist + (size_t)fo * m;
         const int c = fcnt[fo];
         hit = c > 0;
-        for (int x = 0; x < c; ++x) {
+        int x = 0;
+        for (; x + 4 <= c; x += 4) {                    // four list entries' reads in flight
+          int z4[4];
+          double t4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) z4[u] = lst[x + u];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) t4[u] = ab * (er[z4[u]] * T[z4[u] * R + l]) * is2;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) g += t4[u];
+        }
+        for (; x < c; ++x) {
           const int z = lst[x];
           g += ab * (er[z] * T[z * R + l]) * is2;
         }
