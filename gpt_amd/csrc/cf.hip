@@ -3,12 +3,14 @@
 //
 // Model: rating(user, movie) ≈ a · sumUᵀ w sumV with sumU = U[user] + b·Σ U[user's feature rows],
 // sumV = V[movie] + c·Σ V[movie's feature rows] (U: (n1+D1) × r, V: (n2+D2) × r, w: r × r).
-// One workgroup runs a whole epoch of one chain (fold): per minibatch the ratings' sums and
-// residuals are formed in LDS, the gradient rows (users / movies in the batch and their feature
-// rows) are summed in rating order — deterministic, no atomics — into zeroed dense gradient
-// buffers, and then every row of U and V takes its SGD / SGLD step (the prior term moves all
-// rows) or the Stiefel projection + geodesic.  A second kernel predicts every train / test
-// rating after the epoch (running averages, cutoff, squared errors per block).
+// Per minibatch, one workgroup per chain (fold) forms the ratings' sums and residuals in LDS, the
+// w step, and the gradient rows (users / movies in the batch and their feature rows) summed in
+// rating order — deterministic, no atomics — into zeroed dense gradient buffers; then every row of
+// U and V takes its SGD / SGLD step (the prior term moves all rows): for the Euclidean variants in
+// a row-parallel launch over the whole GPU (cf_move_kernel), for the Stiefel ones (projection +
+// geodesic, Grams over every row) inside the same workgroup, which then runs the whole epoch.  A
+// second kernel predicts every train / test rating after the epoch (running averages, cutoff,
+// squared errors per block).
 #include "device_util.h"
 
 namespace gpt {
