@@ -56,6 +56,26 @@ def test_fullw_sideinfo_matches_oracle(name):
     assert np.all(np.abs(got[5] - want[5]) <= 1e-9 * want[5])
 
 
+@pytest.mark.parametrize("lang", [False, True])
+def test_fullw_sideinfo_wide_side_information(lang):
+    """More than 64 side-information columns per side (synthetic 0/1 features appended to the
+    ml-100k ones: 28 + 40 user, 18 + 50 movie columns) take the kernel's CSR path instead of the
+    64-bit feature masks; against the oracle."""
+    from gpt_amd import movielens
+    tr, te, ud, md, mu, sd = problem(3000, 1000)
+    rng = np.random.default_rng(11)
+    ud2 = np.hstack([ud, (rng.random((ud.shape[0], 40)) < 0.05).astype(np.float64)])
+    md2 = np.hstack([md, (rng.random((md.shape[0], 50)) < 0.05).astype(np.float64)])
+    assert ud2.shape[1] > 64 and md2.shape[1] > 64
+    w0 = np.random.default_rng(5).standard_normal((4, 4))
+    args = (tr, ud2, md2, te, 0.8, 0.1, 1.0, w0, 100, 1e-4, 1e-6, 0.5, 0.25, 0.5, 0, 2, 17, mu, sd)
+    got = movielens.GPT_fullw_sideinfo(*args, langevin=lang)
+    want = M.GPT_fullw_sideinfo(*args, langevin=lang)
+    for g, w_ in zip(got[:3], want[:3]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    assert np.all(np.abs(got[5] - want[5]) <= 1e-9 * want[5])
+
+
 def test_fullw_sideinfo_live_config_full_fold():
     """The live run of :723-730 (r = 15, m = 100, SGD, a/b/c = 0.5/0.25/0.5) for one epoch of
     fold 1 (80 000 ratings), against the oracle."""
