@@ -398,6 +398,31 @@ def movielens_main(args):
     ep_us = 1e3 * tm["epoch_ms"] / max(tm["epochs"], 1)
     steps_per_launch = tm["fold_steps"] / max(tm["epochs"], 1)
     achieved = bstep * steps_per_launch / (ep_us * 1e-6) / 1e9
+    # config 5's other sampler (BASELINE: "full-W Gibbs vs SGLD"): GPT_fullw_gibbs on fold 1 with
+    # the parameter line of :743-752 (signal_var = σ_u = 0.5, σ_w = ‖w_init‖_F / r, burnin 15,
+    # avg = true, param_seed 10) at r = 20, timed on the wall clock (whole sweeps, host
+    # bookkeeping included), with the running-average test RMSE beside fullWresults.h5's (r = 15)
+    gibbs = None
+    if rank == 0:
+        tr1, te1, ud1, md1, mu1, sd1 = folds[0]
+        wg = np.random.default_rng(10).standard_normal((r, r))
+        sw_g = math.sqrt((wg ** 2).sum()) / r
+        gsweeps = args.gibbs_sweeps
+        movielens.GPT_fullw_gibbs(tr1, ud1, md1, te1, 0.5, 0.5, sw_g, wg, 1, 2, 1, 10, mu1, sd1,
+                                  avg=True)                       # warm-up
+        tg = time.perf_counter()
+        go = movielens.GPT_fullw_gibbs(tr1, ud1, md1, te1, 0.5, 0.5, sw_g, wg, 15, gsweeps, 1, 10,
+                                       mu1, sd1, avg=True)
+        dtg = time.perf_counter() - tg
+        refg = np.load(os.path.join(ROOT, "tests", "golden", "ref_curves.npz"))["fullW_testRMSE"]
+        curve = np.asarray(go[5])
+        gibbs = {"sampler": "GPT_fullw_gibbs (100k_movielensExperiment.jl:1032-1129), fold 1, r=%d" % r,
+                 "sweeps": 15 + gsweeps, "seconds": dtg, "sweeps_per_s": (15 + gsweeps) / dtg,
+                 "ms_per_sweep": 1e3 * dtg / (15 + gsweeps),
+                 "test_rmse_running_avg_final": float(curve[-1]),
+                 "test_rmse_running_avg_min": float(curve.min()),
+                 "reference_fullWresults_h5_r15": {"at_same_sweep": float(refg[min(gsweeps, len(refg)) - 1]),
+                                                    "final_1000": float(refg[-1]), "min": float(refg.min())}}
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = movielens_cpu_baseline(folds[0], w0, cfg)
@@ -434,6 +459,7 @@ def movielens_main(args):
             "test_rmse": float(np.mean(mins)),
             "test_rmse_note": "meantestRMSE of :735-737: mean over the folds of each fold's minimum "
                               "per-epoch test RMSE (rating units, predictions cut off to [1, 5])",
+            "gibbs": gibbs,
             "quality": {"min_test_rmse_per_fold": mins,
                         "epochs_run_per_fold": [int((o[4] > 0).sum()) for o in outs],
                         "final_train_rmse_per_fold": [float(o[4][o[4] > 0][-1]) if (o[4] > 0).any()
@@ -470,6 +496,8 @@ def main():
                          "(kin40kExperiment.jl's n=150, r=20), powerplant (config 2) or movielens "
                          "(config 5: GPT_fullw_sideinfo over the 5 ml-100k folds)")
     ap.add_argument("--warmup-epochs", type=int, default=2, help="movielens: warm-up call's epochs")
+    ap.add_argument("--gibbs-sweeps", type=int, default=200,
+                    help="movielens: kept sweeps of the full-W Gibbs leg (after 15 burn-in)")
     ap.add_argument("--n", type=int, default=None, help="default: the workload's (500 / 150)")
     ap.add_argument("--D", type=int, default=None, help="default: the workload's D (8 / 4)")
     ap.add_argument("--r", type=int, default=None, help="default: the workload's (5 / 20)")
