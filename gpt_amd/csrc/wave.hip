@@ -429,6 +429,7 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
                    512);
   }
   __syncthreads();
+  if (wv == 0) WSTAMP(srow, 4);
   // V[q,i] = Π_k temp[k, I[q,k], i] in k order (computeV) and w_q·V partial sums of fhat:
   // lanes = batch rows, waves = slices of the core entries
   const int i = lane, ic = min(lane, Bt - 1);
@@ -439,6 +440,16 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
     auto vq = [&](int q) {
       const unsigned short* to = toff_l + q * D;
       double x = 1.0;
+      if (D == 8) {                                   // the 8 offsets of q in one 16-B read
+        const uint4 o4 = *(const uint4*)to;
+        const unsigned ow[4] = {o4.x, o4.y, o4.z, o4.w};
+        double t8[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) t8[kk] = temp_l[((ow[kk >> 1] >> (16 * (kk & 1))) & 0xffffu) + ic];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) x *= t8[kk];
+        return x;
+      }
       for (int k0 = 0; k0 < D; k0 += 8) {
         double t8[8];
 #pragma unroll

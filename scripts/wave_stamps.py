@@ -68,10 +68,11 @@ def main():
     res["expm_2r"] = {"X0+poly": float(np.median(e[:, 12] - e[:, 7])), "solve": float(np.median(e[:, 13] - e[:, 12])),
                       "rest": float(np.median(e[:, 8] - e[:, 13]))}
     vrows = np.array([c * (D + 1) + D for c in alive])
-    vp = out[:, vrows, :4].reshape(-1, 4).astype(np.float64)
+    vp = out[:, vrows, :5].reshape(-1, 5).astype(np.float64)
     okv = (vp > 0).all(axis=1)
-    dv = np.diff(vp[okv], axis=1)
+    dv = np.diff(vp[okv][:, :4], axis=1)
     res["vphase_cycles_median"] = {nm: float(np.median(dv[:, i])) for i, nm in enumerate(VPH)}
+    res["vphase_stage_cycles_median"] = float(np.median(vp[okv][:, 4] - vp[okv][:, 0]))
     # launch spans (first entry to last exit, per step) in shader ticks
     spans = []
     for st in range(args.steps):
