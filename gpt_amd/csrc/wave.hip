@@ -97,7 +97,8 @@ __device__ __forceinline__ double blk_id(int lane, int x, int y) {
 // one pass spilled ~1 400 VGPRs.)  Returns false (nothing written) when M is not diagonally
 // dominant.
 template <int NN>
-__device__ __forceinline__ void wv_solve_dd_pass(const double* M, double* X, int xo, int lane) {
+__device__ __forceinline__ void wv_solve_dd_pass(const double* M, double* X, double* Us, int xo,
+                                                 int lane) {
   constexpr int NX = 64 - NN;                            // right-hand sides per pass
   const bool xl = lane >= NN;
   const int xc = min(xo + lane - NN, NN - 1);            // this lane's X column (clamped)
@@ -107,20 +108,29 @@ __device__ __forceinline__ void wv_solve_dd_pass(const double* M, double* X, int
   for (int i = 0; i < NN; ++i) col[i] = xl ? X[i * NN + xc] : M[i * NN + min(lane, NN - 1)];
   double rpv[NN];
 #pragma unroll
-  for (int p = 0; p < NN; ++p) {                        // forward elimination (getrf + L solve)
-    const double rp = rcp_nr(readlane_d(col[p], p));
-    rpv[p] = rp;
+  for (int p = 0; p < NN; ++p) {                        // forward elimination (getrf + L solve):
+    const double rp = rcp_nr(readlane_d(col[p], p));    // each lane scales its own pivot-row
+    rpv[p] = rp;                                         // entry once, so a row update is one
+    const double g = col[p] * rp;                        // broadcast and one FMA
 #pragma unroll
-    for (int i = p + 1; i < NN; ++i) {
-      const double f = readlane_d(col[i], p) * rp;
-      col[i] -= f * col[p];
-    }
+    for (int i = p + 1; i < NN; ++i) col[i] = fma(-readlane_d(col[i], p), g, col[i]);
   }
+  // back substitution, column-oriented: U's columns go to the scratch slot (lane k writes column
+  // k), so U[0..k-1][k] comes as broadcast LDS reads (two entries per read) instead of 2k readlanes
+  if (lane < NN) {
 #pragma unroll
-  for (int k = NN - 1; k >= 0; --k) {                   // back substitution, column-oriented
+    for (int i = 0; i < NN; i += 2) *(double2*)(Us + lane * NN + i) = make_double2(col[i], col[i + 1]);
+  }
+  wave_sync();
+#pragma unroll
+  for (int k = NN - 1; k >= 0; --k) {
     double u[NN];
 #pragma unroll
-    for (int i = 0; i < k; ++i) u[i] = readlane_d(col[i], k);    // U[0..k-1][k] from lane k
+    for (int i = 0; i < k; i += 2) {
+      const double2 u2 = *(const double2*)(Us + k * NN + i);
+      u[i] = u2.x;
+      if (i + 1 < k) u[i + 1] = u2.y;
+    }
     if (xl) {
       col[k] = col[k] * rpv[k];
 #pragma unroll
@@ -137,8 +147,9 @@ __device__ __forceinline__ void wv_solve_dd_pass(const double* M, double* X, int
 }
 
 template <int NN>
-__device__ __forceinline__ bool wv_solve_dd_passes(const double* M, double* X, int lane, int ncols) {
-  static_assert(NN > 32 && NN < 64, "one X column per lane beside M's");
+__device__ __forceinline__ bool wv_solve_dd_passes(const double* M, double* X, double* Us, int lane,
+                                                   int ncols) {
+  static_assert(NN > 32 && NN < 64 && NN % 2 == 0, "one X column per lane beside M's");
   bool dd = true;
   {
     const int lc = min(lane, NN - 1);
@@ -150,7 +161,7 @@ __device__ __forceinline__ bool wv_solve_dd_passes(const double* M, double* X, i
   }
   if (!__all(dd)) return false;
 #pragma unroll 1
-  for (int xo = 0; xo < ncols; xo += 64 - NN) wv_solve_dd_pass<NN>(M, X, xo, lane);
+  for (int xo = 0; xo < ncols; xo += 64 - NN) wv_solve_dd_pass<NN>(M, X, Us, xo, lane);
   return true;
 }
 
@@ -290,7 +301,7 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
   bool solved = false;
   const int nc = si > 0 ? NN : ncols;
   if constexpr (2 * NN <= 64) solved = wave_solve_dd<NN>(S0, S1);
-  else if constexpr (NN <= 64) solved = wv_solve_dd_passes<NN>(S0, S1, lane, nc);
+  else if constexpr (NN <= 64) solved = wv_solve_dd_passes<NN>(S0, S1, S2, lane, nc);
   if (!solved) wave_solve<NN>(S0, S1);
   if (st && lane == 0) st[1] = (long long)__builtin_amdgcn_s_memtime();
   for (int z = 0; z < si; ++z) {

@@ -29,8 +29,7 @@ def main():
     ap.add_argument("--m", type=int, default=50)
     ap.add_argument("--sgd", action="store_true", help="langevin=False (no noise draws)")
     ap.add_argument("--N", type=int, default=10000, help="training rows used (phi footprint)")
-    ap.add_argument("--engine", default="grid", choices=["grid", "chain", "split"])
-    ap.add_argument("--split", type=int, default=2, help="split engine: batch slices S")
+    ap.add_argument("--engine", default="grid", choices=["grid", "chain"])
     args = ap.parse_args()
     import torch
     import bench
@@ -47,8 +46,6 @@ def main():
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     phi = feature_device(tt(Xtr.T), tt(ls), 1.042, math.sqrt(n / Q ** (1 / D)), tt(Z.T), tt(b.T))
     y = tt(ytr)
-    if args.engine == "split":
-        os.environ["GPTSGLD_SPLIT"] = str(args.split)
     s = SGLDSession(phi, y, I, r, Q, m, 1e-5, 1e-8, 0.0476, 0, 3, list(range(1, args.chains + 1)),
                     store=False, langevin=not args.sgd, engine=args.engine)
     s.run(50)
@@ -113,7 +110,7 @@ def main():
                       % ((nm,) + tuple(dx) + (dict(zip(degs.tolist(), cnt.tolist())),)))
         print("event-timed step kernel: %.2f us" % s.time_steps(20))
         return
-    KB = D * (args.split if args.engine == "split" else 1)     # k-blocks per chain
+    KB = D                                                       # k-blocks per chain
     nb = (KB + 1) * args.chains
     out = np.zeros((args.steps, nb, 16), dtype=np.int64)
     check(lib().gpt_sgld_session_stamps(s._h, args.steps, out.ctypes.data_as(C.POINTER(C.c_int64))))
