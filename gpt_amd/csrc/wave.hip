@@ -562,6 +562,11 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
 
 // ---------------------------------------------------------------------------- dimension launch
 // init != 0: only temp of the batch of step t with the stored U (the first step of a run).
+typedef double pd4 __attribute__((ext_vector_type(4)));
+typedef double pd2 __attribute__((ext_vector_type(2)));
+// the dimension wave's U^(k) staging slot (column-major, stride n) at the start of its LDS
+__device__ __forceinline__ double* U_lds_base(double* sm) { return sm; }
+
 template <int R, int J>
 __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
                                                        const ChainDesc* __restrict__ chains,
@@ -635,6 +640,85 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
     }
   };
 
+  // phidotU on the fp64 matrix cores (n even): temp[k][l][i] = Σ_j U[j][l]·φ[row_i][k][j] as
+  // ⌈R/16⌉ × 4 tiles of v_mfma_f64_16x16x4f64 (M = l, N = the ≤ 64 batch rows, K = j); A = Uᵀ from
+  // U^(k) staged in LDS (column-major, stride n), B = φ rows straight from memory.  Lane λ feeds
+  // the K pair j0 + 2(λ>>4) + {0,1} of row / column λ&15 as one 16-B read, the halves to two
+  // MFMAs (as pred_temp_mfma_kernel); columns l >= R and rows i >= Bn read clamped addresses and
+  // only feed outputs that are never stored, the K tail j >= n is zeroed on the A side.
+  constexpr int TT = (R + 15) / 16;
+  auto phidotU_mfma = [&](const int32_t* ordn, int Bn, double* tdst) {
+    const int kl = lane >> 4, c16 = lane & 15;
+    const double* pa[TT];
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) pa[tt] = U_lds_base(wv_sm) + (size_t)n * min(16 * tt + c16, R - 1);
+    const __attribute__((address_space(1))) double* pb[4];
+#pragma unroll
+    for (int uu = 0; uu < 4; ++uu)
+      pb[uu] = gptr(phik + (size_t)gptr(ordn)[min(16 * uu + c16, Bn - 1)] * rstride);
+    struct Ops { pd2 a[TT], b[4]; };
+    auto load = [&](int j, Ops& o) {
+      const int jj = min(j, n - 2);
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) {
+        const pd2 v = *(const pd2*)(pa[tt] + jj);
+        o.a[tt] = pd2{j < n ? v[0] : 0.0, j + 1 < n ? v[1] : 0.0};
+      }
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) o.b[uu] = *(const __attribute__((address_space(1))) pd2*)(pb[uu] + jj);
+    };
+    pd4 acc[TT][4];
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) acc[tt][uu] = pd4{0.0, 0.0, 0.0, 0.0};
+    auto mma = [&](const Ops& o) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+          for (int uu = 0; uu < 4; ++uu)
+            acc[tt][uu] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.a[tt][h], o.b[uu][h], acc[tt][uu], 0, 0, 0);
+    };
+    // K chunks of 8 through a ring of 4 operand sets (three chunks' loads in flight under each
+    // chunk's MFMAs); the chunk count is rounded up to the ring (chunks past n have zero A), so
+    // the loop has no branch that would make the compiler wait for every outstanding load
+    constexpr int NB = 4;
+    Ops ring[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) load(8 * q + 2 * kl, ring[q]);
+    const int nch = ((n + 7) / 8 + NB - 1) / NB * NB;
+    for (int c0 = 0; c0 < nch; c0 += NB) {
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        mma(ring[q]);
+        load(8 * (c0 + q + NB) + 2 * kl, ring[q]);
+      }
+    }
+    // D[row = kl + 4·reg][col = c16]: row ↔ l, col ↔ batch row
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int l = 16 * tt + kl + 4 * reg, i = 16 * uu + c16;
+          if (l < R && i < Bn) gptr_w(tdst)[((size_t)k * R + l) * m + i] = acc[tt][uu][reg];
+        }
+  };
+  // U^(k) rows of the lane's registers into the LDS staging slot (column-major, stride n)
+  auto u_to_lds = [&]() {
+    double* Ul = U_lds_base(wv_sm);
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj)
+      if (jok[jj]) {
+#pragma unroll
+        for (int l = 0; l < R; ++l) Ul[jc[jj] + (size_t)n * l] = u[jj][l];
+      }
+    wave_sync();
+  };
+
   const int e = (int)(t / P.nb), bb = (int)(t - (long long)e * P.nb);
   const int Bt = min(m, P.N - bb * m);
   const int32_t* ord = Cp->order + (size_t)(e & 1) * P.N + (size_t)bb * m;
@@ -643,7 +727,12 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
     for (int jj = 0; jj < J; ++jj)
 #pragma unroll
       for (int l = 0; l < R; ++l) u[jj][l] = jok[jj] ? gptr(Ug)[jc[jj] + (size_t)n * l] : 0.0;
-    phidotU(ord, Bt, Cp->temp + (size_t)(t & 1) * D * R * m);
+    if ((n & 1) == 0) {
+      u_to_lds();
+      phidotU_mfma(ord, Bt, Cp->temp + (size_t)(t & 1) * D * R * m);
+    } else {
+      phidotU(ord, Bt, Cp->temp + (size_t)(t & 1) * D * R * m);
+    }
     return;
   }
   WSTAMP(srow, 1);
@@ -950,8 +1039,15 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
   if (t1 < P.total_steps) {
     const int e1 = (int)(t1 / P.nb), b1 = (int)(t1 - (long long)e1 * P.nb);
     const int B1 = min(m, P.N - b1 * m);
-    phidotU(Cp->order + (size_t)(e1 & 1) * P.N + (size_t)b1 * m, B1,
-            Cp->temp + (size_t)(t1 & 1) * D * R * m);
+    const int32_t* ord1 = Cp->order + (size_t)(e1 & 1) * P.N + (size_t)b1 * m;
+    double* tdst = Cp->temp + (size_t)(t1 & 1) * D * R * m;
+    if ((n & 1) == 0) {
+      wave_sync();                                       // every read of the slot is done
+      u_to_lds();
+      phidotU_mfma(ord1, B1, tdst);
+    } else {
+      phidotU(ord1, B1, tdst);
+    }
   }
   WSTAMP(srow, 11);
 }
