@@ -14,7 +14,7 @@
 //                     without Psi, :276-408), the Langevin drive, proj (:14-16), geod (:19-37: the
 //                     2r × 2r and r × r Padé expm with the matrices in registers and three LDS
 //                     operand slots), the U write, and temp[k] of the NEXT batch (phidotU,
-//                     :193-205) for the next step's V-phase
+//                     :193-205; fp64 MFMA tiles for even n) for the next step's V-phase
 //
 // The kernel boundary carries the V-phase -> gradU dependency and the temp of the next step; an
 // epoch of launches is one hipGraph (capi.hip).  φ rows are read twice per step (gradU here, the
@@ -340,6 +340,18 @@ __device__ __forceinline__ void copy_to_lds(T* dst, const T* src, int cnt, int t
   }
 }
 
+// copy_to_lds of doubles as 16-B pairs when the count and both addresses allow (half the loads,
+// half the memory round trips for the same UNR)
+typedef double dpair __attribute__((ext_vector_type(2)));
+template <int UNR>
+__device__ __forceinline__ void copy_to_lds_d2(double* dst, const double* src, int cnt, int t,
+                                               int nth) {
+  if (((cnt | (int)((uintptr_t)src >> 3) | (int)((uintptr_t)dst >> 3)) & 1) == 0)
+    copy_to_lds<UNR>((dpair*)dst, (const dpair*)src, cnt / 2, t, nth);
+  else
+    copy_to_lds<UNR>(dst, src, cnt, t, nth);
+}
+
 // Wave totals of NV per-lane values (exact-count butterfly) written to dst[0..NV).
 template <int NV>
 __device__ __forceinline__ void wv_sum_to_lds(double (&v)[NV], double* dst, int lane) {
@@ -430,7 +442,7 @@ __global__ __launch_bounds__(512) void wv_vphase_kernel(StepParams P,
   const int32_t* ord = Cp->order + (size_t)(e & 1) * P.N + (size_t)b * m;
   {
     const double* tsrc = Cp->temp + (size_t)(t & 1) * D * R * m;
-    copy_to_lds<8>(temp_l, tsrc, D * R * m, tid, 512);
+    copy_to_lds_d2<8>(temp_l, tsrc, D * R * m, tid, 512);
     const double* wsrc = Cp->w + (size_t)(t & 1) * Q;
     for (int q = tid; q < Q; q += 512) w_l[q] = gptr(wsrc)[q];
     if (tid == 0) w_l[Q] = 0.0;
@@ -742,8 +754,8 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
   double* cf_l = U_l + n * R;
   double* sctab = wv_sm + wv_dim_lds_dbl(n, R, m);
   sincos_tab_fill(sctab, lane, 64);
-  copy_to_lds<8>(U_l, Ug, n * R, lane, 64);
-  copy_to_lds<8>(cf_l, Cp->coef + (size_t)k * m * R, Bt * R, lane, 64);
+  copy_to_lds_d2<12>(U_l, Ug, n * R, lane, 64);
+  copy_to_lds_d2<8>(cf_l, Cp->coef + (size_t)k * m * R, Bt * R, lane, 64);
   for (int o = Bt * R + lane; o < (Bt + PF - 1) / PF * PF * R; o += 64) cf_l[o] = 0.0;
   wave_sync();
 
