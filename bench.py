@@ -76,6 +76,21 @@ METRICS = {
 }
 KERNELS = {"chain": "chain_kernel<%d,J,2>", "grid": "sgld_step_kernel<%d>",
            "wave": "wv_vphase_kernel<%d> + wv_dim_kernel<%d,J>"}
+KERNEL_LAUNCHES = {"chain": "one chain_kernel launch runs the steps up to the end of an epoch",
+                   "grid": "one sgld_step_kernel launch per step",
+                   "wave": "two launches per step: wv_vphase_kernel, then wv_dim_kernel"}
+KERNEL_US_NOTE = ("device time per step of all chains: one hipEvent pair on the session stream "
+                  "around the %d timed steps' graph launches (kernel gaps inside the graphs "
+                  "included), / steps; %s")
+
+
+def profile_marker(stream):
+    """A ~2 µs spin kernel on `stream`, launched outside the timed region on both sides of it:
+    scripts/prof_timed.py takes the dispatches between the two markers of a kernel trace as the
+    timed steps."""
+    import torch
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(4000)
 
 
 def algorithmic_bytes_per_step(n, D, B, r, Q):
@@ -266,8 +281,8 @@ def compose_line(v):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("%s reference files (tests/golden/%s.npz), whitened; features on device"
-                 % (a.workload, a.workload)),
+        "data": ("the reference's %s files (tests/golden/%s.npz), whitened; features on device"
+                 % (v.dataset, v.dataset)),
         "config": {"workload": v.wdesc, "Ntrain": v.N, "Ntest": v.Nte,
                    "D": v.D, "n_features": v.n, "r": v.r, "Q": v.Q, "minibatch": v.m,
                    "chains_per_gpu": v.C, "chains_alive_after_timed_steps": v.alive,
@@ -280,9 +295,7 @@ def compose_line(v):
                      "kernel": KERNELS[v.info["engine"]].replace("%d", str(v.r)),
                      "kernel_us": v.k_us,
                      "kernel_us_per_rank": v.k_us_ranks,
-                     "kernel_us_note": "per step of all chains; the chain engine runs up to "
-                                       "one epoch of steps per launch (one event pair per "
-                                       "launch, total / steps)",
+                     "kernel_us_note": KERNEL_US_NOTE % (a.steps, KERNEL_LAUNCHES[v.info["engine"]]),
                      "algorithmic_bytes_per_launch": v.bytes_launch,
                      "algorithmic_bytes_per_step": v.bytes_launch,
                      "steps_run_per_chain": v.steps_run}),
@@ -294,7 +307,9 @@ def compose_line(v):
         "pred": {"samples": v.npred, "Ntest": v.Nte, "ms": v.pred_ms, "gemm_flop": v.pred_flop,
                  "achieved_tflops": pred_tfs, "peak_tflops": FP64_MFMA_PEAK_TFS,
                  "frac": pred_tfs / FP64_MFMA_PEAK_TFS,
-                 "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + pred_vphase_pairs_kernel",
+                 "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + %s" % (
+                     "pred_vphase_pairs_kernel" if v.r <= 5 and -(-v.D // 2) <= 8
+                     else "pred_vphase_rows_kernel"),
                  "note": "whole stacked-sample call timed with events (GEMM + V-phase)",
                  "gemm_ms": v.gemm_ms, "vphase_ms": v.vphase_ms,
                  "gemm_roofline": {"bound": "mfma", "achieved": gemm_tfs,
@@ -509,7 +524,6 @@ def main():
     ap.add_argument("--epsw", type=float, default=None, help="default: the workload's")
     ap.add_argument("--epsU", type=float, default=None, help="default: the workload's")
     ap.add_argument("--signal_var", type=float, default=None, help="default: the workload's")
-    ap.add_argument("--kernel-steps", type=int, default=100, help="steps of the event-timed pass")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--clock-warm-ms", type=float, default=300.0,
                     help="untimed GPU clock warm-up on a scratch session before the warmup steps")
@@ -589,16 +603,18 @@ def main():
         # grid engine: D+1 workgroups per chain
         C = ((cus * (2 if D <= 4 else 1)) if eng == "chain"
              else (cus if eng == "wave" else max(1, cus // (D + 1))))
-    need = args.warmup + args.steps + args.kernel_steps
+    need = args.warmup + args.steps
     epochs = -(-need // nb) + 1
     epochs_total = max(args.epochs, epochs)
     last = max(1, min(args.last_epochs, epochs_total))
     seeds = chain_seeds(rank, C)
     # burn-in = all but the last `last` epochs: the timed steps store nothing, the epoch-end
-    # samples of the last epochs feed the converged posterior mean
+    # samples of the last epochs feed the converged posterior mean.  The session runs on a torch
+    # stream of ours, so hipEvents recorded on it bracket exactly the timed steps' launches
+    tstream = torch.cuda.Stream(device=dev)
     sess = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var,
                        epochs_total - last, last, seeds, store_every=nb, store=True,
-                       engine=args.engine)
+                       engine=args.engine, stream=tstream.cuda_stream)
     info = sess.info()
     sess.run(args.warmup)
     sess.prepare(args.steps)           # capture the timed steps' graphs outside the timed region
@@ -626,16 +642,26 @@ def main():
             sw.sync()
             warm_steps += ns
         warm_ms = (time.perf_counter() - tw) * 1000.0
+    # a marker dispatch before and after the timed region (outside it), so a kernel trace of this
+    # command isolates the timed steps' dispatches (scripts/prof_timed.py)
+    profile_marker(tstream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(tstream)
     sess.run(args.steps)
+    ev1.record(tstream)
     sess.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt_rank = time.perf_counter() - t0
+    profile_marker(tstream)
+    # device time of the timed steps on the session stream (the graph launches of the timed
+    # region, gaps between their kernels included): <= the wall time above by construction
+    k_us = 1000.0 * ev0.elapsed_time(ev1) / args.steps
     # chains that hit the geodesic NaN bail-out (GPT_SGLD.jl:422-424) stop stepping; at the
     # reference's own kin40k configuration (εw = 1e-4, εU = 1e-7) about one chain in eight does,
     # as in the reference, and PowerPlant's εw = 5e-5 / εU = 2e-8 loses a few of 512.  Only the
@@ -650,26 +676,26 @@ def main():
     value = total_steps / dt
     ms_per_step = 1000.0 * dt / args.steps
 
-    # per-launch kernel time (hipEvents around each step-kernel launch on the session stream),
-    # right behind the timed steps at the same clock (before the scratch session's free)
-    k_us = sess.time_steps(args.kernel_steps)
-    sess.sync()
     if sw is not None:
         sw.close()
     k_us_ranks = gather_over_ranks(k_us, dev)
-    alive_k = sum(1 for c in range(C) if sess.status(c) == 0)
     B = m
-    bytes_launch = alive_k * algorithmic_bytes_per_step(n, D, B, r, Q)
+    bytes_launch = alive * algorithmic_bytes_per_step(n, D, B, r, Q)
     achieved = bytes_launch / (k_us * 1e-6) / 1e9
     if info["engine"] == "wave":
-        # r = 20: fp64-compute bound (§8(d): ≈42.5 MFLOP against 0.9 MB per chain-step)
-        fl = alive_k * algorithmic_flops_per_step(n, D, B, r, Q)
-        tf = fl / (k_us * 1e-6) / 1e12
-        ex = alive_k * executed_flops_per_step(n, D, B, r, Q)
+        # r = 20: fp64-compute bound.  Primary figure: the flops the engine executes at the Padé
+        # degree these runs take; §8(d)'s count (which prices geod's two expm at 30 (2r)³
+        # products each) beside it
+        fl = alive * algorithmic_flops_per_step(n, D, B, r, Q)
+        ex = alive * executed_flops_per_step(n, D, B, r, Q)
+        tf = ex / (k_us * 1e-6) / 1e12
         roof = {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": tf / FP64_PEAK_TFLOPS, "algorithmic_flops_per_step": fl,
-                "executed_flops_per_step": ex,
-                "executed_frac": ex / (k_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS,
+                "frac": tf / FP64_PEAK_TFLOPS, "flops_per_step": ex,
+                "flops_basis": "executed (Padé degree 5 / 3, r right-hand sides; "
+                               "bench.executed_flops_per_step)",
+                "survey_8d_flops_per_step": fl,
+                "survey_8d_frac": fl / (k_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS,
+                "survey_8d_note": "SURVEY §8(d) count, pricing each expm at 30 (2r)^3 products",
                 "hbm_achieved_GBs": achieved, "hbm_frac": achieved / HBM_PEAK_GBS}
     else:
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -770,14 +796,17 @@ def main():
 
     single = None
     if args.single_chain and rank == 0:
+        s1st = torch.cuda.Stream(device=dev)
         s1 = SGLDSession(phi_tr, y_tr, I, r, Q, m, args.epsw, args.epsU, args.signal_var, 0,
-                         epochs, [7], store_every=nb, store=False, engine=args.engine)
+                         epochs, [7], store_every=nb, store=False, engine=args.engine,
+                         stream=s1st.cuda_stream)
         s1.run(args.warmup)
         s1.prepare(args.steps)
         s1.sync()
-        t1 = time.perf_counter(); s1.run(args.steps); s1.sync()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t1 = time.perf_counter(); e0.record(s1st); s1.run(args.steps); e1.record(s1st); s1.sync()
         sps = args.steps / (time.perf_counter() - t1)
-        s1_us = s1.time_steps(min(args.kernel_steps, s1.total_steps - s1.steps_done))
+        s1_us = 1000.0 * e0.elapsed_time(e1) / args.steps
         b1 = algorithmic_bytes_per_step(n, D, m, r, Q)
         single = {"steps_per_s": sps, "engine": s1.info()["engine"], "kernel_us": s1_us,
                   "roofline_frac": (b1 / (s1_us * 1e-6) / 1e9 / HBM_PEAK_GBS) if s1_us else None}
@@ -799,6 +828,7 @@ def main():
             args=args, value=value, world=world, world_seen=world_seen, warm_ms=warm_ms,
             ms_per_step=ms_per_step, wdesc=wdesc, N=N, Nte=Nte, D=D, n=n, r=r, Q=Q, m=m, C=C,
             info=info, roof=roof, alive=alive, traffic=traffic, traffic_src=traffic_src, k_us=k_us,
+            dataset=loader.__name__,
             k_us_ranks=k_us_ranks, bytes_launch=bytes_launch, steps_run=steps_run, cpu=cpu,
             quality=quality, allreduce_ms=allreduce_ms, npred=npred, pred_ms=pred_ms,
             pred_flop=pred_flop, gemm_ms=gemm_ms, vphase_ms=vphase_ms, rmse_final=rmse_final,

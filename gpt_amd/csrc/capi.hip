@@ -214,6 +214,13 @@ struct gpt_sgld_session {
   DevMem runq;
   DevMem wvtab;                       // wave engine: run members and starts (wave_tables)
   DevMem vtab;                        // grid engine: vphase_cols tables
+  // Bounded in-flight work (gpt_sgld_session_run): an event after every chunk it enqueues, and
+  // before the chunk that would put more than max_inflight chunks (<= one epoch each) in the
+  // stream, a wait for the oldest.  A 200-epoch run() used to enqueue all 200 epoch graphs
+  // (80 000 kernel dispatches on the wave engine) before the first finished.
+  int max_inflight = 8;               // GPTSGLD_MAX_INFLIGHT; 0 = unbounded
+  std::vector<hipEvent_t> inflight;
+  long long chunks_enqueued = 0;
 };
 
 // Engine choice: store_flags bit 2 (or bit 4 / 5, w-only steps / classification) forces the grid
@@ -245,11 +252,13 @@ static int pick_engine(const gpt_sgld_config* c, const int32_t* I_host, int32_t 
       step_layout((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m).bytes <= 160 * 1024;
   const bool wave_ok = wave_supported((int)c->n, (int)c->D, (int)c->r, (int)c->Q, (int)c->m,
                                       c->langevin != 0, c->stiefel != 0);
+  if (flags & 64) { set_error("the split engine (store_flags bit 6) was removed"); return GPT_ERR_BAD_DIMS; }
+  // explicit store_flags win over the environment: bits 4/16/32 (RMSprop-capable sessions, w-only
+  // steps, classification) exist only on the grid engine
   int want = -1;
   if (flags & (4 | 16 | 32)) want = kEngineGrid;
   else if (flags & 8) want = kEngineChain;
   else if (flags & 128) want = kEngineWave;
-  if (flags & 64) { set_error("the split engine (store_flags bit 6) was removed"); return GPT_ERR_BAD_DIMS; }
   else if (const char* ev = std::getenv("GPTSGLD_ENGINE")) {
     if (!std::strcmp(ev, "grid")) want = kEngineGrid;
     else if (!std::strcmp(ev, "chain")) want = kEngineChain;
@@ -509,6 +518,7 @@ extern "C" int gpt_sgld_session_create(const gpt_sgld_config* cfg, int32_t nchai
                             s->total_steps, s->tbase.as<long long>(), 0, 0, s->ord_ws.as<int32_t>(),
                             s->stream));
   s->graph_steps = (int)std::min<long long>(std::max<long long>(s->numbatches, 1), 512);
+  if (const char* ev = std::getenv("GPTSGLD_MAX_INFLIGHT")) s->max_inflight = std::max(0, std::atoi(ev));
   *out = s.release();
   return GPT_OK;
 }
@@ -638,6 +648,26 @@ static int session_next_chunk(const gpt_sgld_session* s, long long remaining, lo
   return (int)std::min<long long>(remaining, to_epoch_end);
 }
 
+// Before enqueueing a chunk: wait until fewer than max_inflight chunks are outstanding.
+static int session_throttle(gpt_sgld_session* s) {
+  if (s->max_inflight <= 0) return GPT_OK;
+  if (s->inflight.empty()) {
+    s->inflight.assign(s->max_inflight, nullptr);
+    for (auto& e : s->inflight) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  if (s->chunks_enqueued >= s->max_inflight)
+    HIPCHK(hipEventSynchronize(s->inflight[s->chunks_enqueued % s->max_inflight]));
+  return GPT_OK;
+}
+
+// After enqueueing a chunk: mark its end in the ring slot the throttle waits on later.
+static int session_mark(gpt_sgld_session* s) {
+  if (s->max_inflight <= 0) return GPT_OK;
+  HIPCHK(hipEventRecord(s->inflight[s->chunks_enqueued % s->max_inflight], s->stream));
+  ++s->chunks_enqueued;
+  return GPT_OK;
+}
+
 extern "C" int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps) {
   if (!s) { set_error("null session"); return GPT_ERR_BAD_DIMS; }
   long long remaining = std::min<long long>(nsteps, s->total_steps - s->steps_done);
@@ -647,6 +677,10 @@ extern "C" int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps) {
     if (rc != GPT_OK) return rc;
   }
   while (remaining > 0) {
+    {
+      const int rc = session_throttle(s);
+      if (rc != GPT_OK) return rc;
+    }
     const int chunk = session_next_chunk(s, remaining, s->steps_done);
     // a whole canonical chunk, or any chunk prepared beforehand (gpt_sgld_session_prepare), runs as
     // one graph; other partial chunks are launched directly
@@ -665,6 +699,10 @@ extern "C" int gpt_sgld_session_run(gpt_sgld_session* s, int64_t nsteps) {
     }
     s->steps_done += chunk;
     remaining -= chunk;
+    {
+      const int rc = session_mark(s);
+      if (rc != GPT_OK) return rc;
+    }
   }
   return GPT_OK;
 }
@@ -930,6 +968,7 @@ extern "C" void gpt_sgld_session_destroy(gpt_sgld_session* s) {
   if (!s) return;
   (void)hipStreamSynchronize(s->stream);
   session_drop_graphs(s);
+  for (auto e : s->inflight) if (e) (void)hipEventDestroy(e);
   if (s->own_stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -1616,7 +1655,7 @@ static int cf_sgd_run(
          f.testpred_store && f.trainRMSE && f.testRMSE && f.N >= 1 && f.Ntest >= 1 &&
          f.ldr >= f.N && f.ldt >= f.Ntest && f.N == folds[0].N;
   if (!ok) { set_error(std::string("bad ") + name + " arguments"); return GPT_ERR_BAD_DIMS; }
-  if (!cf_rank_supported((int)r) || cf_lds_bytes((int)r, (int)m, (int)(D1 + D2)) > 160 * 1024) {
+  if (!cf_rank_supported((int)r) || cf_lds_bytes((int)r, (int)m, (int)(D1 + D2), D1 <= 64 && D2 <= 64) > 160 * 1024) {
     set_error(std::string(name) + ": rank not instantiated (1-6,8,10,12,15,16,20) or minibatch too large");
     return GPT_ERR_BAD_DIMS;
   }

@@ -713,9 +713,12 @@ hipError_t launch_cfg_kron(int r, const double* U, int n1, const double* V, int 
   return hipGetLastError();
 }
 
-size_t cf_lds_bytes(int r, int m, int nfeat) {
+// The per-feature rating lists (fcnt, flist) sit last in the batch carve and exist only on the
+// bitmask path (D1, D2 <= 64); the CSR path sizes them to zero.
+size_t cf_lds_bytes(int r, int m, int nfeat, bool masks) {
+  const size_t lists = masks ? 4 * (size_t)nfeat + 2 * (size_t)nfeat * m : 0;
   const size_t base = 8 * (2 * (size_t)r * r + 4 * (size_t)m * r + m) + 16 * (size_t)m +
-                      4 * (4 * (size_t)m + 2) + 4 * (size_t)nfeat + 2 * (size_t)nfeat * m + 16;
+                      4 * (4 * (size_t)m + 2) + lists + 16;
   const size_t nn = 2 * (size_t)r;
   const size_t stf = 8 * (3 * (size_t)r * r + 7 * nn * nn + 7 * (size_t)r * r + nn * r + r) + 16;
   const size_t moves = 8 * 2 * (size_t)r * r + stf;      // w | wn | Stiefel scratch over the batch
@@ -735,7 +738,7 @@ bool cf_rank_supported(int r) {
 
 hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
                            int bt0, int nb, int domove, hipStream_t st) {
-  const size_t lds = cf_lds_bytes(P.r, P.m, P.D1 + P.D2);
+  const size_t lds = cf_lds_bytes(P.r, P.m, P.D1 + P.D2, P.D1 <= 64 && P.D2 <= 64);
   switch (P.r) {
 #define CASE(RR)                                                                              \
   case RR: {                                                                                  \

@@ -1,0 +1,41 @@
+#!/bin/bash
+# One GPU session of round-5 checks, each step under its own time limit; a test failure (rc 1) is
+# logged and the session goes on, a time limit / abort / segfault (124, 137, 134, 139) ends it.
+#   bash scripts/gpu_r5.sh TAG STEP...
+# Output: gpurun_out/TAG_<step>.log (+ profiles under gpurun_out/TAG_prof_*)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+T=$1; shift
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+PYT="python -u -m pytest -m gpu -q -x --timeout 200 --timeout-method thread"
+run() {   # run NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/${T}_${name}.log" 2>&1
+  local rc=$?
+  tail -4 "gpurun_out/${T}_${name}.log" | grep -v amdgpu.ids
+  echo "== $name rc=$rc"
+  case $rc in 124|137|134|139) exit $rc ;; esac
+  return 0
+}
+RP="rocprofv3 --kernel-trace --stats --output-format csv"
+for s in "$@"; do
+  case $s in
+    tests)   run tests 400 $PYT tests ;;
+    newtests) run newtests 300 $PYT tests/test_gpu_parity.py tests/test_gpu_movielens.py -k "environment or selection or movielens or cf" ;;
+    repro0)  run repro0 300 env GPTSGLD_MAX_INFLIGHT=0 $RP -d gpurun_out/${T}_prof_repro0 -o repro -- python -u scripts/refprof_repro.py --maps gpurun_out/${T}_repro0_maps.txt ;;
+    repro8)  run repro8 300 $RP -d gpurun_out/${T}_prof_repro8 -o repro -- python -u scripts/refprof_repro.py --maps gpurun_out/${T}_repro8_maps.txt ;;
+    bench)   run bench 300 python -u bench.py ;;
+    prof)    run prof 600 $RP -d gpurun_out/${T}_prof_bench -o bench -- python -u bench.py --no-cpu-baseline ;;
+    sweep500) run sweep500 600 python -u scripts/kin40k_step_sweep.py --n 500 --r 5 --epsw 5e-6,1e-5,1.2e-5,1e-4 --epsU 1e-8,3e-8,1e-7,3e-7 --out gpurun_out/${T}_sweep500.json ;;
+    sweep150) run sweep150 600 python -u scripts/kin40k_step_sweep.py --n 150 --r 5 --epsw 5e-6,1e-5,3e-5,1e-4 --epsU 1e-8,3e-8,1e-7,3e-7 --out gpurun_out/${T}_sweep150.json ;;
+    sweep150r20) run sweep150r20 600 python -u scripts/kin40k_step_sweep.py --n 150 --r 20 --epsw 1e-5,3e-5,1e-4,2e-4 --epsU 1e-8,3e-8,1e-7,3e-7 --out gpurun_out/${T}_sweep150r20.json ;;
+    ref)     run ref 600 python -u bench.py --workload kin40k_ref ;;
+    refprof) run refprof 600 $RP -d gpurun_out/${T}_prof_ref -o ref -- python -u bench.py --workload kin40k_ref --no-cpu-baseline ;;
+    ml)      run ml 300 python -u bench.py --workload movielens ;;
+    mlprof)  run mlprof 600 $RP -d gpurun_out/${T}_prof_ml -o ml -- python -u bench.py --workload movielens --no-cpu-baseline ;;
+    pp)      run pp 300 python -u bench.py --workload powerplant ;;
+    quality) run quality 900 $PYT tests/test_gpu_quality.py tests/test_gpu_fullsize.py ;;
+    *) echo "unknown step $s" ;;
+  esac
+done

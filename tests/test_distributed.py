@@ -116,7 +116,7 @@ def test_bench_line_fields_at_world_2():
     args = types.SimpleNamespace(workload="kin40k", steps=20, warmup=5, epsw=1e-5, epsU=1e-8,
                                  signal_var=0.0476)
     quality = dict(test_rmse=0.28, note="x")
-    common = dict(args=args, value=5.0e6, warm_ms=300.0, ms_per_step=0.1, wdesc="kin40k", N=10000,
+    common = dict(args=args, value=5.0e6, warm_ms=300.0, dataset="kin40k", ms_per_step=0.1, wdesc="kin40k", N=10000,
                   Nte=30000, D=8, n=500, r=5, Q=200, m=50, C=256, alive=256,
                   info=dict(engine="chain", workgroups=256, threads=512, lds_bytes=73600),
                   roof={"bound": "hbm", "achieved": 5000.0, "peak": 8000.0, "unit": "GB/s", "frac": 0.625}, traffic=4.2e8, traffic_src="t", bytes_launch=4.94e8,
@@ -133,3 +133,5 @@ def test_bench_line_fields_at_world_2():
     assert two["roofline"]["kernel_us_per_rank"] == [93.0, 94.0]
     assert two["single_chain"]["steps_per_s"] == 2e4
     assert two["config"]["parallelism"] == "chains256x2"
+    assert "tests/golden/kin40k.npz" in two["data"]
+    assert two["pred"]["kernels"].endswith("pred_vphase_pairs_kernel")

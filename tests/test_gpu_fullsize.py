@@ -148,7 +148,8 @@ def test_fullsize_chain_stiefel_invariant_200_epochs(problem):
 def test_r20_wave_stiefel_invariant_and_independence():
     """kin40kExperiment.jl's shape (n = 150, r = 20, εw = 1e-4, εU = 1e-7) on the wave engine with
     256 chains for 20 epochs (4 000 steps): surviving chains stay on the manifold (<= 1e-10),
-    and chain 0 equals a one-chain session of its seed bit for bit."""
+    and the first surviving chain equals a one-chain session of its seed bit for bit (ADVICE r4:
+    the independence check runs whichever chains bail out)."""
     import torch
     import bench
     from gpt_amd import GPT_SGLD as G
@@ -169,13 +170,15 @@ def test_r20_wave_stiefel_invariant_and_independence():
     alive = [c for c in range(256) if s.status(c) == 0]
     assert len(alive) >= 128, len(alive)
     err = _gram_err(s, 256, n2, r2, D)
+    c0 = alive[0]
     U_all = torch.empty((1, n2 * r2 * D), dtype=torch.float64, device="cuda")
     w_all = torch.empty((1, Q), dtype=torch.float64, device="cuda")
-    s.gather_state(0, 1, w_all, U_all)
+    s.gather_state(c0, 1, w_all, U_all)
     s.sync()
     s.close()
     assert err[alive].max() <= 1e-10, err[alive].max()
-    s1 = SGLDSession(phi, y, I, r2, Q, m, 1e-4, 1e-7, SV, 0, 20, [1], store=False, engine="wave")
+    s1 = SGLDSession(phi, y, I, r2, Q, m, 1e-4, 1e-7, SV, 0, 20, [c0 + 1], store=False,
+                     engine="wave")
     s1.run(20 * nb)
     s1.sync()
     U1 = torch.empty_like(U_all)
@@ -184,6 +187,5 @@ def test_r20_wave_stiefel_invariant_and_independence():
     s1.sync()
     st = s1.status(0)
     s1.close()
-    if 0 in alive:
-        assert st == 0
-        assert torch.equal(U1, U_all) and torch.equal(w1, w_all)
+    assert st == 0
+    assert torch.equal(U1, U_all) and torch.equal(w1, w_all)

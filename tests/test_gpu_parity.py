@@ -574,6 +574,37 @@ def test_engine_selection():
             (C.c_void_p * 1)(y.data_ptr()), I.ctypes.data_as(_lib.P_I32), 1 | 64, None, C.byref(h)))
 
 
+@pytest.mark.parametrize("env_engine", ["chain", "wave"])
+def test_explicit_engine_flags_beat_environment(monkeypatch, env_engine):
+    """GPTSGLD_ENGINE applies only when no engine bit is set: w-only steps (bit 16),
+    classification (bit 32) and an explicit grid request (bit 2) stay on the grid engine, the only
+    one that implements them, and still match the oracle."""
+    import torch
+    from gpt_amd.session import SGLDSession
+    monkeypatch.setenv("GPTSGLD_ENGINE", env_engine)
+    n, D, N, r, Q, m, burnin, maxepoch, eps = WONLY_CASES["small"]
+    p = make_problem(n, D, N, r, Q, seed=17)
+    ws, U, gn = G().GPT_SGLDERMw(p["phi"], p["y"], 0.05, p["I"], r, Q, m, eps, burnin, maxepoch,
+                                 31, diag=True)
+    wo, Uo, info = R.GPT_SGLDERMw(p["phi"], p["y"], 0.05, p["I"], r, Q, m, eps, burnin, maxepoch,
+                                  31, record=True)
+    assert rel(ws, wo) < 1e-9 and rel(U, Uo) < 1e-14
+    n, D, N, r, Q, m, ncls, burnin, maxepoch, lang, stf = CLS_CASES["binary_sgld_stiefel"]
+    p = make_problem(n, D, N, r, Q, seed=23)
+    f = p["y"] - np.median(p["y"])
+    y = (1 + np.clip(np.floor((f - f.min()) / (np.ptp(f) + 1e-12) * ncls), 0, ncls - 1)).astype(float)
+    ws, Us = G().GPTclassification(p["phi"], y, p["I"], r, Q, m, 1e-4, 1e-6, burnin, maxepoch, 41)
+    wo, Uo, _ = R.GPTclassification(p["phi"], y, p["I"], r, Q, m, 1e-4, 1e-6, burnin, maxepoch, 41)
+    assert rel(ws, wo) < 1e-8 and rel(Us, Uo) < 1e-8
+    n, D, N, r, Q, m = 32, 4, 60, 3, 12, 16
+    p = make_problem(n, D, N, r, Q, seed=21)
+    phi = torch.from_numpy(np.ascontiguousarray(p["phi"].transpose(2, 1, 0))).cuda()
+    s = SGLDSession(phi, torch.from_numpy(p["y"]).cuda(), p["I"], r, Q, m, 1e-4, 1e-6, 0.05, 0, 1,
+                    [3], engine="grid")
+    assert s.info()["engine"] == "grid"
+    s.close()
+
+
 def test_chain_engine_declines_odd_n_past_one_block():
     """Odd n > 64 cannot use the chain engine's 16-B row staging: forcing it fails loudly
     (GPT_ERR_BAD_DIMS) and the default selection runs the grid engine (n101_odd above)."""

@@ -139,6 +139,69 @@ def test_kin40k_reference_configuration_tracks_reference_curve():
     assert np.all(final >= 0.85 * ref[-1]) and np.all(final <= 1.2 * ref[-1]), final
 
 
+def test_kin40k_bench_shape_converged_quality():
+    """The headline metric's "+ test RMSE" at its own shape (n = 500, D = 8, r = 5, Q = 200,
+    m = 50, the bench's step pair, chain engine), 32 chains over the reference's 200 epochs.  No
+    reference curve exists at r = 5; the bands come from the round-5 sweep (scripts/
+    kin40k_step_sweep.py, profiles/r5c_kin40k_sweep*.json, other chain seeds): at r = 5 the median
+    chain's epoch-200 RMSE sits at 0.344-0.36 for every stable (εw, εU) pair and for n = 150 as
+    well as n = 500, while r = 20 at n = 150 reaches 0.238-0.243 at the same pairs (the reference:
+    0.2385) — the gap to the reference is the rank's capacity, not mixing.  Bands: no bail-out;
+    the median chain's epoch-200 value and last-50 curve mean within [0.33, 0.38]; every chain
+    below its own epoch-1 value; the ensemble of the last 50 epoch-end samples of all chains at
+    most 0.30."""
+    import torch
+    import bench
+    from gpt_amd import GPT_SGLD as G
+    from gpt_amd.session import SGLDSession, feature_device, pred_device
+    dev = torch.device("cuda", 0)
+    _, D, m, ls, srbf, sv, _, n, r, epsw, epsU = bench.WORKLOADS["kin40k"]
+    Q, epochs, chains = 200, 200, 32
+    Xtr, ytr, Xte, yte, ysd = bench.kin40k(D)
+    Nte = Xte.shape[0]
+    nb = -(-Xtr.shape[0] // m)
+    I = G.samplenz(r, D, Q, 17)
+    Z, b = G.feature_inputs(n, D, 17)
+    scale = math.sqrt(n / Q ** (1.0 / D))
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    phi = feature_device(tt(Xtr.T), tt(np.array(ls)), srbf, scale, tt(Z.T), tt(b.T))
+    phite = feature_device(tt(Xte.T), tt(np.array(ls)), srbf, scale, tt(Z.T), tt(b.T))
+    sess = SGLDSession(phi, tt(ytr), I, r, Q, m, epsw, epsU, sv, 0, epochs,
+                       list(range(5001, 5001 + chains)), store_every=nb, store=True,
+                       engine="chain")
+    sess.run(epochs * nb)
+    sess.sync()
+    I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
+    yte_d = tt(yte)
+    fh = torch.empty((epochs, Nte), dtype=torch.float64, device=dev)
+    fsum = torch.zeros(Nte, dtype=torch.float64, device=dev)
+    curves, bailed = [], 0
+    for c in range(chains):
+        if sess.status(c) != 0:
+            bailed += 1
+            continue
+        _, _, ws, Us, ns = sess.device_state(c)
+        assert ns == epochs
+        pred_device(ws, Us, I0, phite, n, D, Nte, r, Q, epochs, fh)
+        err = fh - yte_d[None, :]
+        curves.append((ysd * torch.sqrt((err * err).mean(dim=1))).cpu().numpy())
+        fsum += fh[-50:].sum(dim=0)
+    sess.close()
+    assert bailed == 0, bailed
+    curves = np.array(curves)
+    fmean = (fsum / (50 * chains)).cpu().numpy()
+    ens = float(ysd * math.sqrt(np.mean((fmean - yte) ** 2)))
+    final, last50 = curves[:, -1], curves[:, -50:].mean(axis=1)
+    _record("kin40k_bench_shape", dict(chains=chains, epsw=epsw, epsU=epsU, final=final.tolist(),
+                                       last50_curve_mean=last50.tolist(), ensemble_rmse=ens,
+                                       median_final=float(np.median(final)),
+                                       median_last50=float(np.median(last50))))
+    assert 0.33 <= np.median(final) <= 0.38, np.median(final)
+    assert 0.33 <= np.median(last50) <= 0.38, np.median(last50)
+    assert np.all(final < curves[:, 0])
+    assert ens <= 0.30, ens
+
+
 def test_gpnt_sgld_config1_powerplant_full_run():
     from bench import powerplant
     from gpt_amd import GPT_SGLD as G
@@ -256,12 +319,15 @@ def test_powerplant_config2_converged_tracks_reference_curve():
     the bench's old pair εw = 1e-5, εU = 1e-8 lands +3.1 % high, εU <= 3e-9 too little U motion
     (+4-8 %), εU >= 1e-7 too much noise (+3-6 %, bail-outs), the best stable pair εw = 5e-5,
     εU = 2e-8 +1.1 % — within the spread of the random-feature draw itself (feature seeds 17-21:
-    +1.1 % to +2.2 % at one pair).  16 chains at that pair.  Bands: at most one bail-out; the
-    median chain's last-50-epoch curve mean within 2 % of 4.146 and its epoch-200 value within
-    3 % of 4.145; every chain within [0.95, 1.08]x of the reference's epoch-200 value and below
-    its own epoch-1 value."""
+    +1.1 % to +2.2 % at one pair).  16 chains at that pair, with chain seeds 101-116: the sweep
+    picked the pair on seeds 1-8, so these bands are not fitted to the chains they test (ADVICE
+    r4).  Bands: at most one bail-out — the measured rate at this pair is 4 of 512 chains
+    (profiles/r4pp_bench.json), so a 16-chain run sees one with probability ≈ 12 % and two with
+    ≈ 0.6 %; the median chain's last-50-epoch curve mean within 2 % of 4.146 and its epoch-200
+    value within 3 % of 4.145; every chain within [0.95, 1.08]x of the reference's epoch-200 value
+    and below its own epoch-1 value."""
     ref = np.load(os.path.join(ROOT, "tests", "golden", "ref_curves.npz"))["testRMSE_PP"]
-    curves, bailed = _pp_curves(list(range(1, 17)), 200, 5e-5, 2e-8)
+    curves, bailed = _pp_curves(list(range(101, 117)), 200, 5e-5, 2e-8)
     final, last50 = curves[:, -1], curves[:, -50:].mean(axis=1)
     _record("powerplant_config2", dict(chains=16, bailed=bailed, final=final.tolist(),
                                        last50_curve_mean=last50.tolist(),
