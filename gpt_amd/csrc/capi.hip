@@ -2106,17 +2106,18 @@ static int cf_gibbs_run(
   }
   const int p = (int)rr;
   const int neval = (int)((std::max(N, Ntest) + 255) / 256);
-  DevMem d_tu, d_tm, d_tr, d_eu, d_em, d_er, d_up, d_mp, d_ul, d_ml, d_w, d_U, d_V, d_A, d_M, d_x,
-      d_z, d_trp, d_tep, d_sse, d_st, d_ch, d_zu, d_zv;
+  DevMem d_tu, d_tm, d_tr, d_eu, d_em, d_er, d_up, d_mp, d_ul, d_ml, d_w, d_U, d_V, d_M, d_x,
+      d_z, d_trp, d_tep, d_sse, d_st, d_ch, d_zu, d_zv, d_ws, d_keep;
   HIPCHK(d_tu.alloc(4 * N)); HIPCHK(d_tm.alloc(4 * N)); HIPCHK(d_tr.alloc(8 * N));
   HIPCHK(d_eu.alloc(4 * Ntest)); HIPCHK(d_em.alloc(4 * Ntest)); HIPCHK(d_er.alloc(8 * Ntest));
   HIPCHK(d_up.alloc(4 * uptr.size())); HIPCHK(d_mp.alloc(4 * mptr.size()));
   HIPCHK(d_ul.alloc(4 * N)); HIPCHK(d_ml.alloc(4 * N));
   HIPCHK(d_w.alloc(8 * rr)); HIPCHK(d_U.alloc(8 * nU)); HIPCHK(d_V.alloc(8 * nV));
-  HIPCHK(d_A.alloc(8 * rr * N)); HIPCHK(d_M.alloc(8 * rr * rr)); HIPCHK(d_x.alloc(8 * rr));
+  HIPCHK(d_M.alloc(8 * rr * rr)); HIPCHK(d_x.alloc(8 * rr));
   HIPCHK(d_z.alloc(8 * rr)); HIPCHK(d_trp.alloc(8 * N)); HIPCHK(d_tep.alloc(8 * Ntest));
   HIPCHK(d_sse.alloc(16 * (size_t)neval)); HIPCHK(d_st.alloc(4)); HIPCHK(d_ch.alloc(sizeof(CfChain)));
   HIPCHK(d_zu.alloc(4 * (n1 + 1))); HIPCHK(d_zv.alloc(4 * (n2 + 1)));
+  HIPCHK(d_ws.alloc(8 * cfg_wsystem_scratch_dbl((int)r, (int)n1)));
   HIPCHK(hipMemcpy(d_tu.p, tu.data(), 4 * N, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_tm.p, tm.data(), 4 * N, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_tr.p, tr.data(), 8 * N, hipMemcpyHostToDevice));
@@ -2153,8 +2154,41 @@ static int cf_gibbs_run(
   std::memset(testpred_store, 0, 8 * (size_t)Ntest * maxepoch);
   std::memset(trainRMSE, 0, 8 * (size_t)maxepoch);
   std::memset(testRMSE, 0, 8 * (size_t)maxepoch);
+  // Kept sweeps are recorded on the device (w | U | V | test prediction | the two RMSEs per sweep,
+  // up to ~1 GiB of sweeps at a time) and copied to the caller's arrays in chunks: no host
+  // synchronisation inside a chunk (the round-4 loop copied and synchronised every sweep).
+  const size_t kb = rr + nU + nV + (size_t)Ntest + 2;              // doubles per kept sweep
+  const int64_t chunkE = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(maxepoch, 1),
+                                                                 (int64_t)((1ull << 27) / kb)));
+  HIPCHK(d_keep.alloc(8 * kb * chunkE));
+  double* kw = d_keep.as<double>();
+  double* kU = kw + rr * chunkE;
+  double* kV = kU + nU * chunkE;
+  double* ktp = kV + nV * chunkE;
+  double* krm = ktp + (size_t)Ntest * chunkE;
+  std::vector<double> rm(2 * (size_t)chunkE);
+  int64_t flushed = 0;                              // kept sweeps already in the caller's arrays
+  auto flush = [&](int64_t upto) -> int {
+    HIPCHK(hipStreamSynchronize(nullptr));
+    int32_t bad = 0;
+    HIPCHK(hipMemcpy(&bad, d_st.p, 4, hipMemcpyDeviceToHost));
+    if (bad) { set_error("PosDefException: a Gibbs precision matrix is not positive definite"); return GPT_ERR_NOT_SPD; }
+    const int64_t c = upto - flushed;
+    if (c <= 0) return GPT_OK;
+    if (w_store) HIPCHK(hipMemcpy(w_store + rr * flushed, kw, 8 * rr * c, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(U_store + nU * flushed, kU, 8 * nU * c, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(V_store + nV * flushed, kV, 8 * nV * c, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(testpred_store + (size_t)Ntest * flushed, ktp, 8 * (size_t)Ntest * c,
+                     hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(rm.data(), krm, 16 * c, hipMemcpyDeviceToHost));
+    for (int64_t s2 = 0; s2 < c; ++s2) {
+      trainRMSE[flushed + s2] = rm[2 * s2];
+      testRMSE[flushed + s2] = rm[2 * s2 + 1];
+    }
+    flushed = upto;
+    return GPT_OK;
+  };
   const double su2 = sigma_u * sigma_u;
-  std::vector<double> sse(2 * (size_t)neval), tp(Ntest);
   int counter = 0;
   uint32_t sweep = 0;
   for (int64_t epoch = 1; epoch <= burnin + maxepoch; ++epoch) {
@@ -2169,39 +2203,39 @@ static int cf_gibbs_run(
                             d_tr.as<double>(), signal_var, su2, seed, sweep, kCfgV,
                             d_st.as<int32_t>(), nullptr);
       if (e == hipSuccess && !fixw)
-        e = launch_cfg_kron((int)r, d_U.as<double>(), (int)n1, d_V.as<double>(), (int)n2,
-                            d_tu.as<int32_t>(), d_tm.as<int32_t>(), (int)N, d_A.as<double>(), nullptr);
+        e = launch_cfg_wsystem((int)r, d_U.as<double>(), (int)n1, d_V.as<double>(), (int)n2,
+                               d_up.as<int32_t>(), d_ul.as<int32_t>(), d_tm.as<int32_t>(),
+                               d_tr.as<double>(), 1.0 / signal_var, 1.0 / (sigma_w * sigma_w),
+                               1.0 / signal_var, d_ws.as<double>(), d_M.as<double>(),
+                               d_x.as<double>(), nullptr);
       if (e == hipSuccess && !fixw)
-        e = gaussian_draw_dense(d_A.as<double>(), p, N, d_tr.as<double>(), 1.0 / signal_var,
-                                1.0 / (sigma_w * sigma_w), 1.0 / signal_var, seed, sweep, kCfgW, 0,
-                                d_M.as<double>(), d_x.as<double>(), d_z.as<double>(),
-                                d_w.as<double>(), d_st.as<int32_t>(), nullptr);
+        e = gaussian_draw_prec(d_M.as<double>(), p, d_x.as<double>(), seed, sweep, kCfgW, 0,
+                               d_z.as<double>(), d_w.as<double>(), d_st.as<int32_t>(), nullptr);
       if (e != hipSuccess) return hip_fail(e, name);
     }
-    int32_t bad = 0;
-    HIPCHK(hipMemcpy(&bad, d_st.p, 4, hipMemcpyDeviceToHost));
-    if (bad) { set_error("PosDefException: a Gibbs precision matrix is not positive definite"); return GPT_ERR_NOT_SPD; }
     if (epoch > burnin) {
-      const int64_t s2 = epoch - burnin - 1;
-      if (w_store) HIPCHK(hipMemcpy(w_store + rr * s2, d_w.p, 8 * rr, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(U_store + nU * s2, d_U.p, 8 * nU, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(V_store + nV * s2, d_V.p, 8 * nV, hipMemcpyDeviceToHost));
+      const int64_t s2 = epoch - burnin - 1, slot = (s2 - flushed);
+      if (w_store) HIPCHK(hipMemcpyAsync(kw + rr * slot, d_w.p, 8 * rr, hipMemcpyDeviceToDevice, nullptr));
+      HIPCHK(hipMemcpyAsync(kU + nU * slot, d_U.p, 8 * nU, hipMemcpyDeviceToDevice, nullptr));
+      HIPCHK(hipMemcpyAsync(kV + nV * slot, d_V.p, 8 * nV, hipMemcpyDeviceToDevice, nullptr));
       if (!avg) counter = 0;
       hipError_t e = launch_cf_eval(P, d_ch.as<CfChain>(), 1, (int)std::max(N, Ntest), counter,
                                     nullptr);
+      if (e == hipSuccess)
+        e = launch_cfg_keep(d_ch.as<CfChain>(), (int)Ntest, neval, krm + 2 * slot,
+                            ktp + (size_t)Ntest * slot, nullptr);
       if (e != hipSuccess) return hip_fail(e, "cf eval kernel");
-      HIPCHK(hipMemcpy(sse.data(), d_sse.p, 16 * (size_t)neval, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(tp.data(), d_tep.p, 8 * Ntest, hipMemcpyDeviceToHost));
-      double st0 = 0.0, st1 = 0.0;
-      for (int z = 0; z < neval; ++z) { st0 += sse[2 * z]; st1 += sse[2 * z + 1]; }
-      trainRMSE[s2] = std::sqrt(st0 / (double)N);
-      testRMSE[s2] = std::sqrt(st1 / (double)Ntest);
-      for (int64_t i = 0; i < Ntest; ++i)
-        testpred_store[(size_t)Ntest * s2 + i] = std::min(std::max(tp[i] * ytrainStd + ytrainMean, 1.0), 5.0);
       counter += 1;
+      if (slot + 1 == chunkE) {
+        const int rc = flush(s2 + 1);
+        if (rc != GPT_OK) return rc;
+      }
+    } else if (epoch % 64 == 0) {           // a long burn-in still reports a non-SPD draw early
+      const int rc = flush(flushed);
+      if (rc != GPT_OK) return rc;
     }
   }
-  return GPT_OK;
+  return flush(maxepoch);
 }
 
 extern "C" int gpt_cf_fullw_gibbs(

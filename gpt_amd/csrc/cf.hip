@@ -571,9 +571,16 @@ __global__ __launch_bounds__(256) void cf_eval_kernel(CfParams P, const CfChain*
 // ============================================================================ GPT_fullw_gibbs
 // 100k_movielensExperiment.jl:1032-1129.  One wave per user (side 0) / movie (side 1): the
 // conditional of its row given the other side and w — X = V[Ni,:]·wᵀ (users) or U[Nj,:]·w
-// (movies) streamed rating by rating, precision XᵀX/σ² + I/σ_u², in-wave Cholesky, row =
-// chol(·,:U) \ z + (precision \ Xᵀy)/σ² (:1063-1070, :1077-1084).  status = 1: not SPD.
-template <int R>
+// (movies), precision XᵀX/σ² + I/σ_u², in-wave Cholesky, row = chol(·,:U) \ z +
+// (precision \ Xᵀy)/σ² (:1063-1070, :1077-1084).  status = 1: not SPD.
+// The row's ratings go in chunks of 64: lane λ gathers rating zc + λ's other-side row and forms
+// its X row (all 64 gathers in flight; the round-4 kernel formed one X row at a time behind two
+// dependent global loads, 0.84 ms per launch for the movie with the most ratings), the rows wait
+// in LDS, then the precision / right-hand side accumulate rating by rating in the same order and
+// with the same fma chains as before (identical doubles).
+// MODE 1 (w | U, V statistics, no draw): X = V[Ni,:] itself; writes H_u = Σ_i V[m_i,:]ᵀV[m_i,:]
+// (R², entry a + R·a') and h_u = Σ_i y_i V[m_i,:] (R) per user, zeros for a user without ratings.
+template <int R, int MODE>
 __global__ __launch_bounds__(256) void cfg_rows_kernel(int side, const double* __restrict__ W,
                                                        const double* __restrict__ Oth, int rows_oth,
                                                        double* __restrict__ Me, int rows_me,
@@ -583,42 +590,104 @@ __global__ __launch_bounds__(256) void cfg_rows_kernel(int side, const double* _
                                                        const double* __restrict__ y,
                                                        double signal_var, double su2,
                                                        uint64_t seed, uint32_t sweep,
-                                                       uint32_t stream, int32_t* __restrict__ status) {
+                                                       uint32_t stream, int32_t* __restrict__ status,
+                                                       double* __restrict__ Hout,
+                                                       double* __restrict__ hout) {
   constexpr int NE = (R * R + 63) / 64;
-  __shared__ double Ls[4][R * R], xs[4][R], rh[4][R], zs[4][R];
+  __shared__ double Ls[4][R * R], rh[4][R], zs[4][R], Ws[R * R];
+  __shared__ double Xs[4][64 * R + 64];             // a chunk's X rows | their y
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (MODE == 0)
+    for (int e = threadIdx.x; e < R * R; e += 256) Ws[e] = W[e];
+  __syncthreads();
   const int ent = blockIdx.x * 4 + wv;
   if (ent >= rows_me) return;                       // whole waves only: no block barriers below
   const int z0 = ptr[ent], z1 = ptr[ent + 1];
-  if (z0 == z1) return;                             // no ratings: the row is left as it is
-  double* A = Ls[wv];
-  double* x = xs[wv];
   double acc[NE];
 #pragma unroll
   for (int t = 0; t < NE; ++t) acc[t] = 0.0;
   double racc = 0.0;
-  for (int z = z0; z < z1; ++z) {
-    const int ri = lst[z], o = other[ri];
-    if (lane < R) {
-      double s2 = 0.0;
-      if (side == 0) {
+  if (MODE == 0 && z0 == z1) return;                // no ratings: the row is left as it is
+  double* X = Xs[wv];
+  double* Y = X + 64 * R;
+  // this lane's precision entries e = lane + 64t as (row, column) offsets into an X row; entries
+  // past R² read X[0]·X[0] and are never stored (no branch inside the rating loop)
+  int oa[NE], ob[NE];
 #pragma unroll
-        for (int b = 0; b < R; ++b) s2 = fma(Oth[o + (size_t)rows_oth * b], W[lane + R * b], s2);
+  for (int t = 0; t < NE; ++t) {
+    const int e = min(lane + 64 * t, R * R);
+    oa[t] = e < R * R ? e % R : 0;
+    ob[t] = e < R * R ? e / R : 0;
+  }
+  const int ol = lane < R ? lane : 0;
+  for (int zc = z0; zc < z1; zc += 64) {
+    const int cnt = min(64, z1 - zc);
+    if (lane < cnt) {
+      const int ri = lst[zc + lane], o = other[ri];
+      double orow[R];
+#pragma unroll
+      for (int b = 0; b < R; ++b) orow[b] = Oth[o + (size_t)rows_oth * b];
+      if (MODE == 1) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) X[lane * R + a] = orow[a];
+      } else if (side == 0) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          double s2 = 0.0;
+#pragma unroll
+          for (int b = 0; b < R; ++b) s2 = fma(orow[b], Ws[a + R * b], s2);
+          X[lane * R + a] = s2;
+        }
       } else {
 #pragma unroll
-        for (int a = 0; a < R; ++a) s2 = fma(Oth[o + (size_t)rows_oth * a], W[a + R * lane], s2);
+        for (int a = 0; a < R; ++a) {
+          double s2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < R; ++k) s2 = fma(orow[k], Ws[k + R * a], s2);
+          X[lane * R + a] = s2;
+        }
       }
-      x[lane] = s2;
+      Y[lane] = y[ri];
     }
     wave_sync();
+    // ratings in order (the same fma chain per entry as rating-by-rating), four per pass so their
+    // LDS reads are in flight together
+    int zz = 0;
+    for (; zz + 4 <= cnt; zz += 4) {
+      double xa[4][NE], xb[4][NE], xl[4], yy[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double* x = X + (zz + q) * R;
+#pragma unroll
+        for (int t = 0; t < NE; ++t) { xa[q][t] = x[oa[t]]; xb[q][t] = x[ob[t]]; }
+        xl[q] = x[ol];
+        yy[q] = Y[zz + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int t = 0; t < NE; ++t) acc[t] = fma(xa[q][t], xb[q][t], acc[t]);
+        racc = fma(xl[q], yy[q], racc);
+      }
+    }
+    for (; zz < cnt; ++zz) {
+      const double* x = X + zz * R;
+#pragma unroll
+      for (int t = 0; t < NE; ++t) acc[t] = fma(x[oa[t]], x[ob[t]], acc[t]);
+      racc = fma(x[ol], Y[zz], racc);
+    }
+    wave_sync();
+  }
+  if (MODE == 1) {
 #pragma unroll
     for (int t = 0; t < NE; ++t) {
       const int e = lane + 64 * t;
-      if (e < R * R) acc[t] = fma(x[e % R], x[e / R], acc[t]);
+      if (e < R * R) Hout[(size_t)ent * R * R + e] = acc[t];
     }
-    if (lane < R) racc = fma(x[lane], y[ri], racc);
-    wave_sync();
+    if (lane < R) hout[(size_t)ent * R + lane] = racc;
+    return;
   }
+  double* A = Ls[wv];
 #pragma unroll
   for (int t = 0; t < NE; ++t) {
     const int e = lane + 64 * t;
@@ -629,21 +698,32 @@ __global__ __launch_bounds__(256) void cfg_rows_kernel(int side, const double* _
     zs[wv][lane] = normal_at(seed, (uint32_t)lane, sweep, stream, (uint32_t)ent);
   }
   wave_sync();
+  // lower Cholesky with lane i holding row i (A[i + R·k]); pivots and multipliers broadcast by
+  // v_readlane — the column loop's operations in its order (identical doubles)
   bool bad = false;
-  for (int j = 0; j < R; ++j) {                     // lower Cholesky in place (A[i + R·k], i >= k)
-    const double d = A[j + R * j];
-    bad |= !(d > 0.0);
-    const double pv = sqrt(d);
-    wave_sync();
-    if (lane == 0) A[j + R * j] = pv;
-    if (lane > j && lane < R) A[lane + R * j] /= pv;
-    wave_sync();
-    for (int e = lane; e < R * R; e += 64) {
-      const int i = e % R, k = e / R;
-      if (k > j && i >= k) A[i + R * k] -= A[i + R * j] * A[k + R * j];
+  {
+    double rw[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) rw[k] = A[ol + R * k];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const double d = readlane_d(rw[j], j);
+      bad |= !(d > 0.0);
+      const double pv = sqrt(d);
+      if (lane == j) rw[j] = pv;
+      if (lane > j) rw[j] /= pv;
+#pragma unroll
+      for (int k = j + 1; k < R; ++k) {
+        const double lkj = readlane_d(rw[j], k);
+        if (lane >= k) rw[k] -= rw[j] * lkj;
+      }
     }
-    wave_sync();
+    if (lane < R)
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        if (k <= lane) A[lane + R * k] = rw[k];
   }
+  wave_sync();
   if (lane == 0) {
     if (bad) *status = 1;
     double* rb = rh[wv];
@@ -666,15 +746,104 @@ __global__ __launch_bounds__(256) void cfg_rows_kernel(int side, const double* _
   }
 }
 
-// Kron[:, i] = kron(V[movie_i,:], U[user_i,:]) as the r² × N design of w (:1087-1090).
+// The w | U, V precision without the N × R² Kronecker design (:1088-1092): grouping the ratings
+// by user, Kronᵀ·Kron[(a,b), (a',b')] = Σ_i V[m_i,a]U[u_i,b]V[m_i,a']U[u_i,b'] =
+// Σ_u H_u[a,a']·U[u,b]U[u,b'], i.e. Z = Hᵀ·P with H (n1 × R², MODE-1 rows) and P_u = U[u,:]ᵀU[u,:]
+// (n1 × R²): a GEMM with K = n1 (0.3 GFLOP at r = 20 against the 12.8 GFLOP SYRK of the 256 MB
+// design).  Block = a 64 × 64 tile of Z over one K slice (blockIdx.z), 4 × 4 outputs per thread;
+// partial tiles go to Zp[slice] and cfg_wprec_fin_kernel adds the slices in order.
+constexpr int kWpTile = 64, kWpKc = 16, kWpSlices = 4;
 template <int R>
-__global__ void cfg_kron_kernel(const double* __restrict__ U, int n1, const double* __restrict__ V,
-                                int n2, const int32_t* __restrict__ users,
-                                const int32_t* __restrict__ movies, int N, double* __restrict__ A) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long long)R * R * N) return;
-  const int i = (int)(e / (R * R)), lk = (int)(e - (long long)i * R * R), l = lk % R, k = lk / R;
-  A[e] = V[movies[i] + (size_t)n2 * k] * U[users[i] + (size_t)n1 * l];
+__global__ __launch_bounds__(256) void cfg_wprec_kernel(const double* __restrict__ H,
+                                                        const double* __restrict__ U, int n1,
+                                                        double* __restrict__ Zp) {
+  constexpr int P = R * R;
+  __shared__ __attribute__((aligned(16))) double Hs[kWpKc][kWpTile], Ps[kWpKc][kWpTile];
+  __shared__ double Us[kWpKc][R];
+  const int tid = threadIdx.x, tr = tid & 15, tc = tid >> 4;
+  const int e0 = blockIdx.x * kWpTile, f0 = blockIdx.y * kWpTile;
+  const int per = (n1 + kWpSlices - 1) / kWpSlices;
+  const int u0 = blockIdx.z * per, u1 = min(n1, u0 + per);
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  for (int uc = u0; uc < u1; uc += kWpKc) {
+    const int cnt = min(kWpKc, u1 - uc);
+    for (int x = tid; x < kWpKc * R; x += 256) {
+      const int k = x / R, b = x - k * R;
+      Us[k][b] = k < cnt ? U[(uc + k) + (size_t)n1 * b] : 0.0;
+    }
+    for (int x = tid; x < kWpKc * kWpTile; x += 256) {
+      const int k = x / kWpTile, c = x - k * kWpTile;
+      Hs[k][c] = (k < cnt && e0 + c < P) ? H[(size_t)(uc + k) * P + e0 + c] : 0.0;
+    }
+    __syncthreads();
+    for (int x = tid; x < kWpKc * kWpTile; x += 256) {
+      const int k = x / kWpTile, c = x - k * kWpTile, f = min(f0 + c, P - 1);
+      Ps[k][c] = Us[k][f % R] * Us[k][f / R];
+    }
+    __syncthreads();
+    for (int k = 0; k < cnt; ++k) {
+      double h[4], q[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { h[i] = Hs[k][tr + 16 * i]; q[i] = Ps[k][tc + 16 * i]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fma(h[i], q[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  double* Z = Zp + (size_t)blockIdx.z * P * P;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + tr + 16 * i, f = f0 + tc + 16 * j;
+      if (e < P && f < P) Z[(size_t)e + (size_t)P * f] = acc[i][j];
+    }
+}
+
+// M[(a·R + b) + p·(a'·R + b')] = alpha·Σ_slices Z[(a + R·a') + p·(b + R·b')] + beta·δ, p = R²
+template <int R>
+__global__ __launch_bounds__(256) void cfg_wprec_fin_kernel(const double* __restrict__ Zp,
+                                                            double alpha, double beta,
+                                                            double* __restrict__ M) {
+  constexpr int P = R * R;
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= P * P) return;
+  const int c = o % P, c2 = o / P;
+  const int a = c / R, b = c - a * R, a2 = c2 / R, b2 = c2 - a2 * R;
+  const size_t zi = (size_t)(a + R * a2) + (size_t)P * (b + R * b2);
+  double s = Zp[zi];
+#pragma unroll
+  for (int sl = 1; sl < kWpSlices; ++sl) s += Zp[(size_t)sl * P * P + zi];
+  M[o] = alpha * s + (c == c2 ? beta : 0.0);
+}
+
+// x[a·R + b] = ysc·Σ_u h_u[a]·U[u,b]  (Kronᵀ·y, :1093), one workgroup, users in order
+template <int R>
+__global__ __launch_bounds__(512) void cfg_wrhs_kernel(const double* __restrict__ hv,
+                                                       const double* __restrict__ U, int n1,
+                                                       double ysc, double* __restrict__ x) {
+  __shared__ double hs[64][R], us[64][R];
+  const int tid = threadIdx.x, a = tid / R, b = tid - a * R;
+  double s = 0.0;
+  for (int uc = 0; uc < n1; uc += 64) {
+    const int cnt = min(64, n1 - uc);
+    for (int e = tid; e < 64 * R; e += 512) {
+      const int k = e / R, l = e - k * R;
+      hs[k][l] = k < cnt ? hv[(size_t)(uc + k) * R + l] : 0.0;
+      us[k][l] = k < cnt ? U[(uc + k) + (size_t)n1 * l] : 0.0;
+    }
+    __syncthreads();
+    if (tid < R * R)
+      for (int k = 0; k < cnt; ++k) s = fma(hs[k][a], us[k][b], s);
+    __syncthreads();
+  }
+  if (tid < R * R) x[tid] = ysc * s;
 }
 
 hipError_t launch_cfg_rows(int side, int r, const double* W, const double* Oth, int rows_oth,
@@ -685,9 +854,9 @@ hipError_t launch_cfg_rows(int side, int r, const double* W, const double* Oth, 
   switch (r) {
 #define CASE(RR)                                                                              \
   case RR:                                                                                    \
-    hipLaunchKernelGGL(cfg_rows_kernel<RR>, dim3((rows_me + 3) / 4), dim3(256), 0, st, side, W, \
-                       Oth, rows_oth, Me, rows_me, ptr, lst, other, y, signal_var, su2, seed,  \
-                       sweep, stream, status);                                                \
+    hipLaunchKernelGGL((cfg_rows_kernel<RR, 0>), dim3((rows_me + 3) / 4), dim3(256), 0, st,   \
+                       side, W, Oth, rows_oth, Me, rows_me, ptr, lst, other, y, signal_var,   \
+                       su2, seed, sweep, stream, status, nullptr, nullptr);                   \
     break;
     GPT_CF_RANKS(CASE)
 #undef CASE
@@ -696,20 +865,62 @@ hipError_t launch_cfg_rows(int side, int r, const double* W, const double* Oth, 
   return hipGetLastError();
 }
 
-hipError_t launch_cfg_kron(int r, const double* U, int n1, const double* V, int n2,
-                           const int32_t* users, const int32_t* movies, int N, double* A,
-                           hipStream_t st) {
-  const long long tot = (long long)r * r * N;
+// w | U, V (GPT_fullw_gibbs :1088-1094): precision M = Kronᵀ·Kron/σ² + I/σ_w² and rhs x =
+// Kronᵀ·y/σ² from per-user statistics.  Scratch: H (n1·r²), h (n1·r), Zp (kWpSlices·r⁴).
+size_t cfg_wsystem_scratch_dbl(int r, int n1) {
+  return (size_t)n1 * r * r + (size_t)n1 * r + (size_t)kWpSlices * r * r * r * r;
+}
+
+hipError_t launch_cfg_wsystem(int r, const double* U, int n1, const double* V, int n2,
+                              const int32_t* uptr, const int32_t* ulst, const int32_t* movies,
+                              const double* y, double alpha, double beta, double ysc,
+                              double* scratch, double* M, double* x, hipStream_t st) {
+  const int p = r * r;
+  double* H = scratch;
+  double* hv = H + (size_t)n1 * p;
+  double* Zp = hv + (size_t)n1 * r;
   switch (r) {
 #define CASE(RR)                                                                              \
   case RR:                                                                                    \
-    hipLaunchKernelGGL(cfg_kron_kernel<RR>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, \
-                       st, U, n1, V, n2, users, movies, N, A);                                \
+    hipLaunchKernelGGL((cfg_rows_kernel<RR, 1>), dim3((n1 + 3) / 4), dim3(256), 0, st, 0,      \
+                       nullptr, V, n2, nullptr, n1, uptr, ulst, movies, y, 1.0, 1.0,          \
+                       (uint64_t)0, 0u, 0u, nullptr, H, hv);                                  \
+    hipLaunchKernelGGL(cfg_wprec_kernel<RR>,                                                  \
+                       dim3((p + kWpTile - 1) / kWpTile, (p + kWpTile - 1) / kWpTile,        \
+                            kWpSlices), dim3(256), 0, st, H, U, n1, Zp);                      \
+    hipLaunchKernelGGL(cfg_wprec_fin_kernel<RR>, dim3((p * p + 255) / 256), dim3(256), 0, st, \
+                       Zp, alpha, beta, M);                                                   \
+    hipLaunchKernelGGL(cfg_wrhs_kernel<RR>, dim3(1), dim3(512), 0, st, hv, U, n1, ysc, x);    \
     break;
     GPT_CF_RANKS(CASE)
 #undef CASE
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// Per sweep kept (GPT_fullw_gibbs / GPT_fixw_gibbs bookkeeping, :1097-1118): the train / test
+// RMSE from the evaluation kernel's block partials (added in block order, as the host used to),
+// and the cut-off de-standardised test prediction of the sweep.
+__global__ __launch_bounds__(256) void cfg_keep_kernel(const CfChain* __restrict__ chains,
+                                                       int neval, double* __restrict__ rmse,
+                                                       double* __restrict__ tp_out) {
+  const CfChain C = chains[0];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < C.Ntest)
+    tp_out[i] = fmin(fmax(C.testpred[i] * C.ystd + C.ymean, 1.0), 5.0);
+  if (i == 0) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int z = 0; z < neval; ++z) { s0 += C.sse[2 * z]; s1 += C.sse[2 * z + 1]; }
+    rmse[0] = sqrt(s0 / (double)C.N);
+    rmse[1] = sqrt(s1 / (double)C.Ntest);
+  }
+}
+
+hipError_t launch_cfg_keep(const CfChain* chains, int Ntest, int neval, double* rmse,
+                           double* tp_out, hipStream_t st) {
+  hipLaunchKernelGGL(cfg_keep_kernel, dim3((Ntest + 255) / 256), dim3(256), 0, st, chains, neval,
+                     rmse, tp_out);
   return hipGetLastError();
 }
 

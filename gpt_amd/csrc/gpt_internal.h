@@ -281,9 +281,15 @@ hipError_t launch_cfg_rows(int side, int r, const double* W, const double* Oth, 
                            const int32_t* other, const double* y, double signal_var, double su2,
                            uint64_t seed, uint32_t sweep, uint32_t stream, int32_t* status,
                            hipStream_t st);
-hipError_t launch_cfg_kron(int r, const double* U, int n1, const double* V, int n2,
-                           const int32_t* users, const int32_t* movies, int N, double* A,
-                           hipStream_t st);
+size_t cfg_wsystem_scratch_dbl(int r, int n1);
+hipError_t launch_cfg_wsystem(int r, const double* U, int n1, const double* V, int n2,
+                              const int32_t* uptr, const int32_t* ulst, const int32_t* movies,
+                              const double* y, double alpha, double beta, double ysc,
+                              double* scratch, double* M, double* x, hipStream_t st);
+hipError_t launch_cfg_keep(const CfChain* chains, int Ntest, int neval, double* rmse,
+                           double* tp_out, hipStream_t st);
+hipError_t gaussian_draw_prec(double* M, int p, double* x, uint64_t seed, uint32_t c1, uint32_t c2,
+                              uint32_t c3, double* z, double* out, int32_t* status, hipStream_t st);
 hipError_t gaussian_draw_dense(const double* A, int p, long long N, const double* y, double alpha,
                                double beta, double ysc, uint64_t seed, uint32_t c1, uint32_t c2,
                                uint32_t c3, double* M, double* x, double* z, double* out,

@@ -130,14 +130,47 @@ __global__ __launch_bounds__(256) void syrk_mfma_kernel(const double* __restrict
   }
 }
 
-// out[a] = alpha · Σ_i A[a + p·i] · y[i]
-__global__ void gemv_kernel(const double* __restrict__ A, int p, long long N,
-                            const double* __restrict__ y, double alpha, double* __restrict__ out) {
-  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+// out[a] = alpha · Σ_i A[a + p·i] · y[i] in two launches: partial sums over column chunks of
+// kGemvCh (threads over a: every load of a column is coalesced; one thread per a, as the round-4
+// kernel had, ran 80 000 serial loads on 2 workgroups: 19.5 ms per MovieLens w draw), then the
+// chunks added in chunk order (deterministic).
+constexpr int kGemvCh = 256;
+__global__ __launch_bounds__(256) void gemv_part_kernel(const double* __restrict__ A, int p,
+                                                        long long N, const double* __restrict__ y,
+                                                        double* __restrict__ part) {
+  const int a = blockIdx.y * 256 + threadIdx.x;
+  const long long i0 = (long long)blockIdx.x * kGemvCh;
+  const int cnt = (int)min((long long)kGemvCh, N - i0);
+  if (a >= p) return;
+  const double* col = A + (size_t)p * i0 + a;
+  double s = 0.0;
+#pragma unroll 8
+  for (int i = 0; i < cnt; ++i) s = fma(col[(size_t)p * i], y[i0 + i], s);
+  part[(size_t)blockIdx.x * p + a] = s;
+}
+__global__ __launch_bounds__(256) void gemv_fin_kernel(const double* __restrict__ part, int p,
+                                                       int nch, double alpha,
+                                                       double* __restrict__ out) {
+  const int a = blockIdx.x * 256 + threadIdx.x;
   if (a >= p) return;
   double s = 0.0;
-  for (long long i = 0; i < N; ++i) s = fma(A[a + (size_t)p * i], y[i], s);
+  for (int c = 0; c < nch; ++c) s += part[(size_t)c * p + a];
   out[a] = alpha * s;
+}
+
+static hipError_t launch_gemv(const double* A, int p, long long N, const double* y, double alpha,
+                              double* out, hipStream_t st) {
+  const int nch = (int)((N + kGemvCh - 1) / kGemvCh);
+  double* part = nullptr;
+  hipError_t e = hipMallocAsync((void**)&part, 8 * (size_t)nch * p, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gemv_part_kernel, dim3(nch, (p + 255) / 256), dim3(256), 0, st, A, p, N, y,
+                     part);
+  hipLaunchKernelGGL(gemv_fin_kernel, dim3((p + 255) / 256), dim3(256), 0, st, part, p, nch, alpha,
+                     out);
+  e = hipGetLastError();
+  (void)hipFreeAsync(part, st);
+  return e;
 }
 
 __global__ void axpy_kernel(double* __restrict__ x, const double* __restrict__ z, int p) {
@@ -159,7 +192,8 @@ __global__ void normals_kernel(double* __restrict__ z, int cnt, uint64_t seed, u
 }
 
 // In-place lower Cholesky of the SPD matrix M (column-major p × p, lower triangle read), one
-// workgroup: right-looking, column by column.  status = 1 if a pivot is not positive.
+// workgroup: right-looking, column by column (p > kCholPMax; chol_blk_kernel below otherwise).
+// status = 1 if a pivot is not positive.
 constexpr int kTgpNT = 1024;
 __global__ __launch_bounds__(kTgpNT) void chol_kernel(double* __restrict__ M, int p,
                                                       int32_t* __restrict__ status) {
@@ -208,6 +242,286 @@ __global__ __launch_bounds__(kTgpNT) void trsv_kernel(const double* __restrict__
   }
 }
 
+// Blocked form for p <= kCholPMax, one workgroup of kTgpNT threads, panels of kCholNB columns
+// (the p = 400 w precision of GPT_fullw_gibbs at r = 20 took 5.3 ms with the column kernel):
+//  1. the panel (rows j0..p-1) -> LDS, rows padded to kCholS doubles (conflict-free per lane row);
+//  2. wave 0 factors the diagonal block in registers (lane i holds row i; pivots and multipliers
+//     broadcast by v_readlane);
+//  3. every thread solves one panel row against it (L21 = A21·L11⁻ᵀ);
+//  4. the trailing lower triangle takes the rank-kCholNB update: a wave task is 64 consecutive
+//     rows (lane = row, its panel row in registers) × 4 consecutive columns (their panel rows read
+//     as LDS broadcasts), a coalesced read-modify-write of M per column.
+// The factor is also written transposed into the upper triangle (Lᵀ, row j of L = column j of
+// the upper part), which the transposed solve reads column-wise (trsv_blk_kernel).
+constexpr int kCholNB = 16;
+constexpr int kCholS = 18;
+constexpr int kCholPMax = 1024;
+#ifndef GPT_CHOL_STAMPS
+#define GPT_CHOL_STAMPS 0
+#endif
+#ifndef GPT_CHOL_EXP
+#define GPT_CHOL_EXP 0              // diagnostic builds: 1 no C loads, 2 no C stores, 3 no MFMA
+#endif
+#if GPT_CHOL_STAMPS
+__device__ long long g_chol_stamps[64 * 8];       // per panel: phase-end shader clocks (thread 0)
+#define CHOL_STAMP(ph) do { if (tid == 0 && j0 / kCholNB < 64) g_chol_stamps[(j0 / kCholNB) * 8 + (ph)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define CHOL_STAMP(ph) do {} while (0)
+#endif
+__global__ __launch_bounds__(kTgpNT) void chol_blk_kernel(double* __restrict__ M, int p,
+                                                          int32_t* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) double Pn[kCholPMax * kCholS];   // 144 KB
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int j0 = 0; j0 < p; j0 += kCholNB) {
+    CHOL_STAMP(0);
+    // a last panel narrower than kCholNB is padded with identity columns: the padded block
+    // factors to [L11 0; 0 I] and its zero columns add nothing below, so no step needs a guard
+    const int nb = min(kCholNB, p - j0), rows = p - j0;
+    for (int e = tid; e < rows * kCholNB; e += kTgpNT) {        // panel -> LDS (coalesced over i)
+      const int jj = e / rows, i = e - jj * rows;
+      Pn[i * kCholS + jj] = jj < nb ? M[(size_t)(j0 + i) + (size_t)p * (j0 + jj)]
+                                    : (i == jj ? 1.0 : 0.0);
+    }
+    __syncthreads();
+    CHOL_STAMP(1);
+    if (wv == 0) {                                               // diagonal block, one wave
+      // dpotf2's form: the pivot's square root, then its reciprocal scales the column
+      double rw[kCholNB];
+#pragma unroll
+      for (int k = 0; k < kCholNB; ++k)
+        rw[k] = lane < nb ? Pn[lane * kCholS + k] : (k == lane ? 1.0 : 0.0);
+      bool bad = false;
+      double rdg = 0.0;                                          // lane j: 1 / L[j][j]
+#pragma unroll
+      for (int j = 0; j < kCholNB; ++j) {
+        const double d = readlane_d(rw[j], j);
+        bad |= !(d > 0.0);
+        const double pv = sqrt(d), rp = 1.0 / pv;
+        if (lane == j) { rw[j] = pv; rdg = rp; }
+        if (lane > j) rw[j] = rw[j] * rp;
+#pragma unroll
+        for (int k = j + 1; k < kCholNB; ++k) {
+          const double lkj = readlane_d(rw[j], k);
+          if (lane >= k) rw[k] -= rw[j] * lkj;
+        }
+      }
+      if (lane == 0 && bad) *status = 1;
+      if (lane < kCholNB) {
+#pragma unroll
+        for (int k = 0; k < kCholNB; ++k) Pn[lane * kCholS + k] = k <= lane ? rw[k] : 0.0;
+        Pn[lane * kCholS + kCholNB] = rdg;                       // the row's pad slot
+      }
+    }
+    __syncthreads();
+    CHOL_STAMP(2);
+    for (int i = kCholNB + tid; i < rows; i += kTgpNT) {        // L21 = A21 · L11⁻ᵀ, a row each
+      double x[kCholNB];
+#pragma unroll
+      for (int j = 0; j < kCholNB; ++j) {
+        double s2 = Pn[i * kCholS + j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s2 -= x[k] * Pn[j * kCholS + k];
+        x[j] = s2 * Pn[j * kCholS + kCholNB];
+      }
+#pragma unroll
+      for (int j = 0; j < kCholNB; ++j) Pn[i * kCholS + j] = x[j];
+    }
+    __syncthreads();
+    CHOL_STAMP(3);
+    for (int e = tid; e < rows * nb; e += kTgpNT) {             // the factored panel -> M (L)
+      const int jj = e / rows, i = e - jj * rows;
+      if (i >= jj) M[(size_t)(j0 + i) + (size_t)p * (j0 + jj)] = Pn[i * kCholS + jj];
+    }
+    for (int e = tid; e < rows * kCholNB; e += kTgpNT) {        // and transposed (Lᵀ), row-wise
+      const int i = e / kCholNB, jj = e - i * kCholNB;
+      if (jj < nb && i >= jj) M[(size_t)(j0 + jj) + (size_t)p * (j0 + i)] = Pn[i * kCholS + jj];
+    }
+    CHOL_STAMP(4);
+    // trailing update of rows / cols j0+16 .. p-1 (lower triangle): C -= L21·L21ᵀ in 16 × 16
+    // tiles on the fp64 matrix cores (v_mfma_f64_16x16x4f64, K = 16 in four steps), one tile
+    // per wave at a time; lane λ feeds L21[tile row λ&15][k0 + (λ>>4)] for both operands and
+    // holds C[(λ>>4) + 4q][λ&15] (as syrk_mfma_kernel)
+    const int rem = rows - kCholNB;
+    if (rem > 0) {
+      // the MFMA computes the tile transposed (first operand from the column tile), so lane λ
+      // holds C[r0 + (λ&15)][c0 + (λ>>4) + 4q]: each load / store of C covers 16 consecutive rows
+      // of 4 columns (a few cache lines) instead of 16 columns
+      const int T = (rem + 15) / 16, npair = T * (T + 1) / 2;
+      const int li = lane & 15, lk = lane >> 4;
+      constexpr int PW = 4;                                      // tiles of a wave in flight
+      for (int t0 = wv; t0 < npair; t0 += PW * (kTgpNT / 64)) {
+        int r0[PW], c0[PW];
+        d4 acc[PW];
+#pragma unroll
+        for (int w4 = 0; w4 < PW; ++w4) {
+          const int t = min(t0 + w4 * (kTgpNT / 64), npair - 1);
+          int ti = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) / 2.0);
+          while (ti * (ti + 1) / 2 > t) --ti;
+          while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+          const int tj = t - ti * (ti + 1) / 2;
+          r0[w4] = kCholNB + 16 * ti;                            // panel-relative
+          c0[w4] = kCholNB + 16 * tj;
+          const int row = r0[w4] + li;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int col = c0[w4] + lk + 4 * q;
+#if GPT_CHOL_EXP == 1
+            acc[w4][q] = 0.0 * row * col;
+#else
+            acc[w4][q] = (row < rows && col < rows) ? M[(size_t)(j0 + row) + (size_t)p * (j0 + col)]
+                                                    : 0.0;
+#endif
+          }
+        }
+#pragma unroll
+        for (int w4 = 0; w4 < PW; ++w4) {
+          const int ra = min(r0[w4] + li, rows - 1), rb = min(c0[w4] + li, rows - 1);
+#pragma unroll
+          for (int s4 = 0; s4 < kCholNB / 4; ++s4) {
+            const double av = -Pn[rb * kCholS + 4 * s4 + lk];
+            const double bv = Pn[ra * kCholS + 4 * s4 + lk];
+#if GPT_CHOL_EXP == 3
+            acc[w4][0] += av * bv;
+#else
+            acc[w4] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[w4], 0, 0, 0);
+#endif
+          }
+        }
+#pragma unroll
+        for (int w4 = 0; w4 < PW; ++w4) {
+          if (t0 + w4 * (kTgpNT / 64) >= npair) break;
+          const int row = r0[w4] + li;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int col = c0[w4] + lk + 4 * q;
+#if GPT_CHOL_EXP == 2
+            if (row < rows && col < rows && row >= col && acc[w4][q] == 12345.678)
+#else
+            if (row < rows && col < rows && row >= col)
+#endif
+              M[(size_t)(j0 + row) + (size_t)p * (j0 + col)] = acc[w4][q];
+          }
+        }
+      }
+    }
+    CHOL_STAMP(5);
+    __syncthreads();
+    CHOL_STAMP(6);
+  }
+}
+
+// x := L⁻¹ x (TRANS = 0) or L⁻ᵀ x (TRANS = 1) after chol_blk_kernel (L in the lower triangle, Lᵀ
+// in the upper one), p <= kCholPMax, one workgroup of 256 threads with x in LDS, in blocks of
+// kCholNB columns: wave 0 solves the block's triangle in registers (lane = row, pivots broadcast
+// by v_readlane), then every thread updates its rows with the block's kCholNB solved values
+// (column-major reads, coalesced over the rows).  The same operations in the same order as the
+// column kernel (trsv_kernel): identical doubles, two block barriers per kCholNB columns instead
+// of two per column.
+template <int TRANS>
+__global__ __launch_bounds__(256) void trsv_blk_kernel(const double* __restrict__ L, int p,
+                                                       double* __restrict__ x) {
+  constexpr int RPT = kCholPMax / 256;              // rows per thread
+  __shared__ double xs[kCholPMax];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < p; i += 256) xs[i] = x[i];
+  const int nblk = (p + kCholNB - 1) / kCholNB;
+  // forward: blocks in order; transposed: from the last block (its rows jb0 .. jb1-1) down
+  auto range = [&](int bi, int& jb0, int& jb1) {
+    jb0 = TRANS ? max(0, p - (bi + 1) * kCholNB) : bi * kCholNB;
+    jb1 = TRANS ? p - bi * kCholNB : min(p, jb0 + kCholNB);
+  };
+  // lane r (< nb) of wave 0 holds row jb0 + r of the block's triangle: forward,
+  // L[jb0+r][jb0+k] (k <= r); transposed, Lᵀ[jb0+r][jb0+k] = L[jb0+k][jb0+r] from the upper part
+  // (k >= r).  Loaded one block ahead.
+  double rw[kCholNB];
+  auto load_tri = [&](int bi) {
+    int jb0, jb1;
+    range(bi, jb0, jb1);
+    const int nb = jb1 - jb0, rr = jb0 + min(lane, nb - 1);
+#pragma unroll
+    for (int k = 0; k < kCholNB; ++k) rw[k] = k < nb ? L[(size_t)rr + (size_t)p * (jb0 + k)] : 1.0;
+  };
+  if (wv == 0) load_tri(0);
+  __syncthreads();
+  for (int bi = 0; bi < nblk; ++bi) {
+    int jb0, jb1;
+    range(bi, jb0, jb1);
+    const int nb = jb1 - jb0;
+    // this thread's rectangle entries, in flight while wave 0 solves the triangle
+    const int r0 = TRANS ? 0 : jb1, r1 = TRANS ? jb0 : p;
+    double lr[RPT][kCholNB];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int i = min(r0 + tid + 256 * u, p - 1);
+#pragma unroll
+      for (int k = 0; k < kCholNB; ++k)
+        lr[u][k] = (k < nb && r0 + tid + 256 * u < r1) ? L[(size_t)i + (size_t)p * (jb0 + k)] : 0.0;
+    }
+    if (wv == 0) {
+      double xv = lane < nb ? xs[jb0 + lane] : 0.0;
+      if (!TRANS) {
+#pragma unroll
+        for (int j = 0; j < kCholNB; ++j) {
+          if (j < nb) {
+            const double xj = readlane_d(xv, j) / readlane_d(rw[j], j);
+            if (lane == j) xv = xj;
+            if (lane > j) xv -= rw[j] * xj;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = kCholNB - 1; j >= 0; --j) {
+          if (j < nb) {
+            const double xj = readlane_d(xv, j) / readlane_d(rw[j], j);
+            if (lane == j) xv = xj;
+            if (lane < j) xv -= rw[j] * xj;
+          }
+        }
+      }
+      if (lane < nb) xs[jb0 + lane] = xv;
+      if (bi + 1 < nblk) load_tri(bi + 1);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int i = r0 + tid + 256 * u;
+      if (i < r1) {
+        double s2 = xs[i];
+        if (!TRANS) {
+#pragma unroll
+          for (int k = 0; k < kCholNB; ++k)
+            if (k < nb) s2 -= lr[u][k] * xs[jb0 + k];
+        } else {
+#pragma unroll
+          for (int k = kCholNB - 1; k >= 0; --k)
+            if (k < nb) s2 -= lr[u][k] * xs[jb0 + k];
+        }
+        xs[i] = s2;
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < p; i += 256) x[i] = xs[i];
+}
+
+static void launch_chol(double* M, int p, int32_t* status, hipStream_t st) {
+  if (p <= kCholPMax)
+    hipLaunchKernelGGL(chol_blk_kernel, 1, kTgpNT, 0, st, M, p, status);
+  else
+    hipLaunchKernelGGL(chol_kernel, 1, kTgpNT, 0, st, M, p, status);
+}
+
+// triangular solve against launch_chol's factor (the blocked forms go together: trsv_blk reads
+// the transposed factor chol_blk leaves in the upper triangle)
+static void launch_trsv(const double* M, int p, double* x, int trans, hipStream_t st) {
+  if (p <= kCholPMax) {
+    if (trans) hipLaunchKernelGGL(trsv_blk_kernel<1>, 1, 256, 0, st, M, p, x);
+    else hipLaunchKernelGGL(trsv_blk_kernel<0>, 1, 256, 0, st, M, p, x);
+  } else {
+    hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, p, x, trans);
+  }
+}
+
 // ------------------------------------------------------------------------------ host side
 #define GPT_TGP_RANKS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(15) X(16) X(20)
 
@@ -253,13 +567,14 @@ hipError_t tgp_gibbs(const double* b, const double* y, int n, int D, long long N
     const int Tq = (q + 15) / 16;
     hipLaunchKernelGGL(syrk_mfma_kernel, nblk((long long)Tq * (Tq + 1) / 2, 4), 256, 0, st, V, q, N,
                        1.0 / s2, 1.0 / sigma_w2, M);
-    hipLaunchKernelGGL(gemv_kernel, nblk(q, 256), 256, 0, st, V, q, N, y, 1.0 / s2, x);
-    hipLaunchKernelGGL(chol_kernel, 1, kTgpNT, 0, st, M, q, status);
-    hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, q, x, 0);
+    e = launch_gemv(V, q, N, y, 1.0 / s2, x, st);
+    if (e != hipSuccess) break;
+    launch_chol(M, q, status, st);
+    launch_trsv(M, q, x, 0, st);
     hipLaunchKernelGGL(normals_kernel, nblk(q, 256), 256, 0, st, z, q, seed, (uint32_t)(it - 1),
                        (uint32_t)kTgpWNoise, 0u);
     hipLaunchKernelGGL(axpy_kernel, nblk(q, 256), 256, 0, st, x, z, q);
-    hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, q, x, 1);   // W = L⁻ᵀ(L⁻¹ rhs + z)
+    launch_trsv(M, q, x, 1, st);   // W = L⁻ᵀ(L⁻¹ rhs + z)
     e = hipMemcpyAsync(W, x, 8 * (size_t)q, hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) break;
     if (it > burnin) {
@@ -279,13 +594,14 @@ hipError_t tgp_gibbs(const double* b, const double* y, int n, int D, long long N
                          k, Ck);
       hipLaunchKernelGGL(syrk_mfma_kernel, nblk((long long)Tu * (Tu + 1) / 2, 4), 256, 0, st, Ck, nr,
                          N, 1.0 / s2, 1.0 / sigma_u2, M);
-      hipLaunchKernelGGL(gemv_kernel, nblk(nr, 256), 256, 0, st, Ck, nr, N, y, 1.0 / s2, x);
+      e = launch_gemv(Ck, nr, N, y, 1.0 / s2, x, st);
+      if (e != hipSuccess) break;
       hipLaunchKernelGGL(normals_kernel, nblk(nr, 256), 256, 0, st, z, nr, seed, (uint32_t)(it - 1),
                          (uint32_t)kTgpUNoise, (uint32_t)k);
       hipLaunchKernelGGL(axpy_kernel, nblk(nr, 256), 256, 0, st, x, z, nr);
-      hipLaunchKernelGGL(chol_kernel, 1, kTgpNT, 0, st, M, nr, status);
-      hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, nr, x, 0);
-      hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, nr, x, 1);   // U_k = M⁻¹(rhs + z)
+      launch_chol(M, nr, status, st);
+      launch_trsv(M, nr, x, 0, st);
+      launch_trsv(M, nr, x, 1, st);   // U_k = M⁻¹(rhs + z)
       e = hipMemcpyAsync(U + (size_t)nr * k, x, 8 * (size_t)nr, hipMemcpyDeviceToDevice, st);
       if (e != hipSuccess) break;
       e = launch_tgp_temp(U, b, n, D, N, r, k, 1, tnew - (size_t)k * r * N, st);
@@ -302,9 +618,23 @@ hipError_t tgp_gibbs(const double* b, const double* y, int n, int D, long long N
   return e;
 }
 
-// out = L⁻ᵀz + ysc·M⁻¹(A·y), M = alpha·A·Aᵀ + beta·I = L·Lᵀ (A: p × N column-major, z on the
-// Philox normal stream (c1, c2, c3)): the Gaussian conditional draw of a linear-Gaussian block
-// (GPT_fullw_gibbs w | U, V, 100k_movielensExperiment.jl:1087-1094).  Scratch: M (p²), x, z (p).
+// out = L⁻ᵀz + M⁻¹x for the SPD precision M = L·Lᵀ (column-major p × p, factored in place) and
+// z on the Philox normal stream (c1, c2, c3): the Gaussian conditional draw of a linear-Gaussian
+// block (GPT_fullw_gibbs w | U, V, 100k_movielensExperiment.jl:1087-1094: mu = M \ rhs, then
+// chol(M,:U) \ randn + mu).  Scratch: x (p, overwritten with the mean), z (p).
+hipError_t gaussian_draw_prec(double* M, int p, double* x, uint64_t seed, uint32_t c1, uint32_t c2,
+                              uint32_t c3, double* z, double* out, int32_t* status, hipStream_t st) {
+  launch_chol(M, p, status, st);
+  launch_trsv(M, p, x, 0, st);
+  launch_trsv(M, p, x, 1, st);          // mu = M⁻¹x
+  hipLaunchKernelGGL(normals_kernel, nblk(p, 256), 256, 0, st, z, p, seed, c1, c2, c3);
+  launch_trsv(M, p, z, 1, st);          // L⁻ᵀz
+  hipLaunchKernelGGL(gmc_sum_kernel, nblk(p, 256), 256, 0, st, z, x, out, p);
+  return hipGetLastError();
+}
+
+// The same draw with M = alpha·A·Aᵀ + beta·I and x = ysc·A·y formed from the dense design A
+// (p × N column-major).  Scratch: M (p²), x, z (p).
 hipError_t gaussian_draw_dense(const double* A, int p, long long N, const double* y, double alpha,
                                double beta, double ysc, uint64_t seed, uint32_t c1, uint32_t c2,
                                uint32_t c3, double* M, double* x, double* z, double* out,
@@ -312,14 +642,9 @@ hipError_t gaussian_draw_dense(const double* A, int p, long long N, const double
   const int T = (p + 15) / 16;
   hipLaunchKernelGGL(syrk_mfma_kernel, nblk((long long)T * (T + 1) / 2, 4), 256, 0, st, A, p, N,
                      alpha, beta, M);
-  hipLaunchKernelGGL(gemv_kernel, nblk(p, 256), 256, 0, st, A, p, N, y, ysc, x);
-  hipLaunchKernelGGL(chol_kernel, 1, kTgpNT, 0, st, M, p, status);
-  hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, p, x, 0);
-  hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, p, x, 1);          // mu = M⁻¹(ysc·A·y)
-  hipLaunchKernelGGL(normals_kernel, nblk(p, 256), 256, 0, st, z, p, seed, c1, c2, c3);
-  hipLaunchKernelGGL(trsv_kernel, 1, kTgpNT, 0, st, M, p, z, 1);          // L⁻ᵀz
-  hipLaunchKernelGGL(gmc_sum_kernel, nblk(p, 256), 256, 0, st, z, x, out, p);
-  return hipGetLastError();
+  hipError_t e = launch_gemv(A, p, N, y, ysc, x, st);
+  if (e != hipSuccess) return e;
+  return gaussian_draw_prec(M, p, x, seed, c1, c2, c3, z, out, status, st);
 }
 
 // ============================================================================ GPT_GMC

@@ -36,6 +36,11 @@ for s in "$@"; do
     mlprof)  run mlprof 600 $RP -d gpurun_out/${T}_prof_ml -o ml -- python -u bench.py --workload movielens --no-cpu-baseline ;;
     pp)      run pp 300 python -u bench.py --workload powerplant ;;
     quality) run quality 900 $PYT tests/test_gpu_quality.py tests/test_gpu_fullsize.py ;;
+    gibbsprof) run gibbsprof 300 $RP -d gpurun_out/${T}_prof_gibbs -o gibbs -- python -u scripts/time_gibbs.py --sweeps 40 ;;
+    pair) run pair 300 python -u bench.py --epsw 1e-4 --epsU 1e-8 --no-cpu-baseline --no-single-chain ;;
+    hq) run hq 300 $PYT tests/test_gpu_quality.py -k "bench_shape or powerplant_config2_converged" ;;
+    mltests) run mltests 400 $PYT tests/test_gpu_movielens.py tests/test_gpu_tgp.py tests/test_gpu_quality.py -k "movielens or tgp or gibbs or bench_shape" ;;
+    gibbs) run gibbs 300 python -u scripts/time_gibbs.py --sweeps 200 ;;
     *) echo "unknown step $s" ;;
   esac
 done
