@@ -368,26 +368,31 @@ __global__ void pred_offs_kernel(const int32_t* __restrict__ I0, int Q, int D, i
   offs[x] = (int32_t)((k * R + I0[q + Q * k]) * 64);
 }
 
-__global__ __launch_bounds__(64) void pred_vphase_rows_kernel(const double* __restrict__ w,
-                                                              const double* __restrict__ T,
-                                                              const int32_t* __restrict__ offs,
-                                                              int D, int R, long long Ntest,
-                                                              int Q, double* __restrict__ fhat) {
+// kRowsWaves waves share one (sample, 64 rows) tile: they stage its D·R temp rows together and
+// split the core entries (contiguous ranges of q), adding their partial sums in wave order.  With
+// one wave per tile (round 4) a tile's 82 KB of LDS at r = 20, D = 8 left one wave per CU: 7.7 ms
+// per 224-sample call, against the 7.1 ms GEMM.
+constexpr int kRowsWaves = 16;
+__global__ __launch_bounds__(64 * kRowsWaves) void pred_vphase_rows_kernel(
+    const double* __restrict__ w, const double* __restrict__ T, const int32_t* __restrict__ offs,
+    int D, int R, long long Ntest, int Q, double* __restrict__ fhat) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* tl = (double*)smem;                       // [k·R + l][64]
-  const int lane = threadIdx.x;
+  double* part = tl + (size_t)D * R * 64;           // [wave][64]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int s = blockIdx.y;
   const long long i0 = (long long)blockIdx.x * 64;
   const long long i = i0 + lane;
   const bool ok = i < Ntest;
   const double* Ts = T + (size_t)s * D * R * Ntest + (ok ? i : i0);
-  for (int row = 0; row < D * R; ++row) tl[row * 64 + lane] = gptr(Ts)[(size_t)row * Ntest];
-  wave_sync();
+  for (int row = wv; row < D * R; row += kRowsWaves) tl[row * 64 + lane] = gptr(Ts)[(size_t)row * Ntest];
+  __syncthreads();
   const auto* ofq = cptr(offs);
   const auto* wq = cptr(w + (size_t)s * Q);
+  const int qa = Q * wv / kRowsWaves, qb = Q * (wv + 1) / kRowsWaves;
   double f0 = 0.0, f1 = 0.0;
-  int q = 0;
-  for (; q + 2 <= Q; q += 2) {
+  int q = qa;
+  for (; q + 2 <= qb; q += 2) {
     double v0 = wq[q], v1 = wq[q + 1];
     for (int k = 0; k < D; ++k) {
       v0 *= tl[ofq[q * D + k] + lane];
@@ -396,12 +401,19 @@ __global__ __launch_bounds__(64) void pred_vphase_rows_kernel(const double* __re
     f0 += v0;
     f1 += v1;
   }
-  if (q < Q) {
+  if (q < qb) {
     double v0 = wq[q];
     for (int k = 0; k < D; ++k) v0 *= tl[ofq[q * D + k] + lane];
     f0 += v0;
   }
-  if (ok) fhat[(size_t)s * Ntest + i] = f0 + f1;
+  part[wv * 64 + lane] = f0 + f1;
+  __syncthreads();
+  if (wv == 0) {
+    double f = part[lane];
+#pragma unroll
+    for (int x = 1; x < kRowsWaves; ++x) f += part[x * 64 + lane];
+    if (ok) fhat[(size_t)s * Ntest + i] = f;
+  }
 }
 
 // V-phase with pair tables: the D factors of V[q, i] are taken two dimensions at a time from
@@ -640,7 +652,7 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
   if (e != hipSuccess) return e;
   int32_t* offs = (int32_t*)((char*)T + tbytes);
   int32_t* offp = offs + (size_t)Q * D;
-  const size_t rlds = 8 * (size_t)D * r * 64;
+  const size_t rlds = 8 * (size_t)D * r * 64 + 8 * (size_t)kRowsWaves * 64;
   // V-phase variant: "pairs" (default where the tables fit: ⌈D/2⌉ ≤ 8 and ≤ 96 KB), "rows", "tile"
   const int vmode = [] {
     const char* ev = std::getenv("GPTSGLD_PRED_VPHASE");
@@ -690,7 +702,7 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
         e = set_max_lds_once((const void*)pred_vphase_rows_kernel, 160 * 1024, attr);
         if (e != hipSuccess) break;
       }
-      hipLaunchKernelGGL(pred_vphase_rows_kernel, vg, dim3(64), rlds, st, w + (size_t)s0 * Q, T,
+      hipLaunchKernelGGL(pred_vphase_rows_kernel, vg, dim3(64 * kRowsWaves), rlds, st, w + (size_t)s0 * Q, T,
                          offs, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest);
       e = hipGetLastError();
       if (timing && e == hipSuccess) {

@@ -41,6 +41,9 @@ for s in "$@"; do
     hq) run hq 300 $PYT tests/test_gpu_quality.py -k "bench_shape or powerplant_config2_converged" ;;
     mltests) run mltests 400 $PYT tests/test_gpu_movielens.py tests/test_gpu_tgp.py tests/test_gpu_quality.py -k "movielens or tgp or gibbs or bench_shape" ;;
     gibbs) run gibbs 300 python -u scripts/time_gibbs.py --sweeps 200 ;;
+    pred20) run pred20 300 python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows ;;
+    pred5) run pred5 300 python -u scripts/time_pred.py --S 256 --tiles 44 --vphases pairs,rows ;;
+    predtests) run predtests 300 $PYT tests/test_gpu_parity.py -k "pred" ;;
     *) echo "unknown step $s" ;;
   esac
 done
