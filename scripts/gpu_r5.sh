@@ -44,6 +44,11 @@ for s in "$@"; do
     pred20) run pred20 300 python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows ;;
     pred5) run pred5 300 python -u scripts/time_pred.py --S 256 --tiles 44 --vphases pairs,rows ;;
     predtests) run predtests 300 $PYT tests/test_gpu_parity.py -k "pred" ;;
+    wavetests) run wavetests 400 $PYT tests/test_gpu_parity.py -k "expm or wave or manifold or selection or injected or nan or multichain or epoch_order" ;;
+    expm) run expm 200 python -u scripts/expm_bench.py --nn 40 ;;
+    wstamps) run wstamps 200 python -u scripts/wave_stamps.py --chains 256 --steps 4 --out gpurun_out/${T}_wstamps.json ;;
+    refq) run refq 300 python -u bench.py --workload kin40k_ref --no-cpu-baseline --epochs 20 ;;
+    mlstamps) run mlstamps 300 python -u scripts/ml_stamps.py ;;
     *) echo "unknown step $s" ;;
   esac
 done
