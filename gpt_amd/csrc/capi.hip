@@ -1790,30 +1790,67 @@ static int cf_sgd_run(
     ~Events() { for (auto x : e) if (x) (void)hipEventDestroy(x); }
   } evs;
   for (auto& x : evs.e) HIPCHK(hipEventCreate(&x));
+  // the run's own stream; the SGD / SGLD path replays one captured graph per epoch (gather + the
+  // epoch's batch-phase / move launch pairs), its steps counted from a device-side epoch base
+  struct RunStream {
+    hipStream_t s = nullptr;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t x = nullptr;
+    ~RunStream() {
+      if (s) (void)hipStreamSynchronize(s);
+      if (x) (void)hipGraphExecDestroy(x);
+      if (g) (void)hipGraphDestroy(g);
+      if (s) (void)hipStreamDestroy(s);
+    }
+  } rs;
+  HIPCHK(hipStreamCreateWithFlags(&rs.s, hipStreamNonBlocking));
+  hipStream_t st = rs.s;
+  HIPCHK(hipStreamSynchronize(nullptr));             // the set-up copies / memsets are done
+  DevMem d_step;
+  HIPCHK(d_step.alloc(sizeof(long long)));
   g_cf_timing = CfTiming{};
   for (int64_t epoch = 1; epoch <= burnin + maxepoch && nlive > 0; ++epoch) {
     host_randperm((int)N, seed, (int)(epoch - 1), perm.data());
     HIPCHK(hipMemcpy(d_perm.p, perm.data(), 4 * N, hipMemcpyHostToDevice));
-    HIPCHK(hipEventRecord(evs.e[0], nullptr));
-    {
-      const hipError_t eg = launch_cf_gather(d_ch.as<CfChain>(), F, (int)N, nullptr);
-      if (eg != hipSuccess) return hip_fail(eg, "cf gather kernel");
-    }
     hipError_t e = hipSuccess;
     if (stiefel) {
       // the Stiefel move needs Grams over every row: the whole epoch in one workgroup per fold
-      e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, (epoch - 1) * nbatch, 0, nbatch, 1, nullptr);
-    } else {
-      // per minibatch: the batch phase (one workgroup per fold), then the row-parallel move of U
-      // and V over the whole GPU (cf_move_kernel)
+      HIPCHK(hipEventRecord(evs.e[0], st));
+      e = launch_cf_gather(d_ch.as<CfChain>(), F, (int)N, st);
+      if (e == hipSuccess)
+        e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, (epoch - 1) * nbatch, 0, nbatch, 1, st);
+    } else if (P.stamps) {
+      // the stamped first epoch: direct launches (the stamp buffer is dropped after it)
+      HIPCHK(hipEventRecord(evs.e[0], st));
+      e = launch_cf_gather(d_ch.as<CfChain>(), F, (int)N, st);
       for (int b = 0; b < nbatch && e == hipSuccess; ++b) {
         const long long step = (epoch - 1) * nbatch + b;
-        e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, step, b, 1, 0, nullptr);
-        if (e == hipSuccess) e = launch_cf_move(P, d_ch.as<CfChain>(), F, step, nullptr);
+        e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, step, b, 1, 0, st);
+        if (e == hipSuccess) e = launch_cf_move(P, d_ch.as<CfChain>(), F, step, st);
       }
+    } else {
+      // per minibatch: the batch phase (one workgroup per fold), then the row-parallel move of U
+      // and V over the whole GPU (cf_move_kernel) — an epoch of them as one graph
+      if (!rs.x) {
+        HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        e = launch_cf_gather(d_ch.as<CfChain>(), F, (int)N, st);
+        for (int b = 0; b < nbatch && e == hipSuccess; ++b) {
+          e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, b, b, 1, 0, st, d_step.as<long long>());
+          if (e == hipSuccess)
+            e = launch_cf_move(P, d_ch.as<CfChain>(), F, b, st, d_step.as<long long>());
+        }
+        const hipError_t ec = hipStreamEndCapture(st, &rs.g);
+        if (e != hipSuccess) return hip_fail(e, "cf epoch capture");
+        if (ec != hipSuccess) return hip_fail(ec, "hipStreamEndCapture");
+        HIPCHK(hipGraphInstantiate(&rs.x, rs.g, nullptr, nullptr, 0));
+      }
+      const long long base = (epoch - 1) * nbatch;
+      HIPCHK(hipMemcpyAsync(d_step.p, &base, sizeof(long long), hipMemcpyHostToDevice, st));
+      HIPCHK(hipEventRecord(evs.e[0], st));
+      e = hipGraphLaunch(rs.x, st);
     }
     if (e != hipSuccess) return hip_fail(e, "cf epoch kernel");
-    HIPCHK(hipEventRecord(evs.e[1], nullptr));
+    HIPCHK(hipEventRecord(evs.e[1], st));
     HIPCHK(hipEventSynchronize(evs.e[1]));
     if (P.stamps) {                // the first epoch only
       g_cf_stamps.resize((size_t)kCfStampSteps * kCfStampSlots);
@@ -1843,10 +1880,10 @@ static int cf_sgd_run(
     if (epoch > burnin && nlive > 0) {
       const int64_t s2 = epoch - burnin - 1;
       if (!avg) counter = 0;
-      HIPCHK(hipEventRecord(evs.e[2], nullptr));
-      e = launch_cf_eval(P, d_ch.as<CfChain>(), F, nmax, counter, nullptr);
+      HIPCHK(hipEventRecord(evs.e[2], st));
+      e = launch_cf_eval(P, d_ch.as<CfChain>(), F, nmax, counter, st);
       if (e != hipSuccess) return hip_fail(e, "cf eval kernel");
-      HIPCHK(hipEventRecord(evs.e[3], nullptr));
+      HIPCHK(hipEventRecord(evs.e[3], st));
       HIPCHK(hipEventSynchronize(evs.e[3]));
       {
         float ms = 0.f;

@@ -203,7 +203,9 @@ __device__ bool cf_move(const CfParams& P, double* M, double* G, int rows, int w
 // workgroup (blockIdx.x = f), whose next batch then reads U and V from its own L2.
 template <int R>
 __global__ __launch_bounds__(256) void cf_move_kernel(CfParams P, const CfChain* chains,
-                                                      long long step, int nchains) {
+                                                      const long long* step_base, long long step,
+                                                      int nchains) {
+  if (step_base) step += *step_base;                 // graph replays: the epoch's first step
   int fold, blk;
   if (nchains <= 8) {
     fold = blockIdx.x & 7;
@@ -255,6 +257,7 @@ __global__ __launch_bounds__(256) void cf_move_kernel(CfParams P, const CfChain*
 // batch of the epoch, step0 its step.
 template <int R>
 __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfChain* chains,
+                                                         const long long* step_base,
                                                          long long step0, int bt0, int nb,
                                                          int domove) {
 
@@ -287,6 +290,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
   // the barrier before the moves until the next batch reloads them (r = 20 fits 160 KB this way)
   double* scr = sU;
   if (__hip_atomic_load(C.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  if (step_base) step0 += *step_base;                // graph replays: the epoch's first step
   for (int o = tid; o < R * R; o += kCfNT) w_l[o] = C.w[o];
   const double is2 = 1.0 / P.signal_var;
   for (int bt = bt0; bt < bt0 + nb; ++bt) {
@@ -948,7 +952,8 @@ bool cf_rank_supported(int r) {
 }
 
 hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
-                           int bt0, int nb, int domove, hipStream_t st) {
+                           int bt0, int nb, int domove, hipStream_t st,
+                           const long long* step_base) {
   const size_t lds = cf_lds_bytes(P.r, P.m, P.D1 + P.D2, P.D1 <= 64 && P.D2 <= 64);
   switch (P.r) {
 #define CASE(RR)                                                                              \
@@ -957,7 +962,7 @@ hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains
     hipError_t e = set_max_lds_once((const void*)cf_epoch_kernel<RR>, 160 * 1024, attr);      \
     if (e != hipSuccess) return e;                                                            \
     hipLaunchKernelGGL(cf_epoch_kernel<RR>, dim3(nchains), dim3(kCfNT), lds, st, P, chains,   \
-                       step0, bt0, nb, domove);                                               \
+                       step_base, step0, bt0, nb, domove);                                    \
   } break;
     GPT_CF_RANKS(CASE)
 #undef CASE
@@ -985,14 +990,15 @@ hipError_t launch_cf_gather(const CfChain* chains, int nchains, int N, hipStream
 }
 
 hipError_t launch_cf_move(const CfParams& P, const CfChain* chains, int nchains, long long step,
-                          hipStream_t st) {
+                          hipStream_t st, const long long* step_base) {
   const int RE = P.r + (P.r & 1);
   const unsigned blocks = (unsigned)(((long long)(P.rowsU + P.rowsV) * (RE / 2) + 255) / 256);
   const dim3 grid = nchains <= 8 ? dim3(8 * blocks) : dim3(blocks, nchains);
   switch (P.r) {
 #define CASE(RR)                                                                              \
   case RR:                                                                                    \
-    hipLaunchKernelGGL(cf_move_kernel<RR>, grid, dim3(256), 0, st, P, chains, step, nchains);  \
+    hipLaunchKernelGGL(cf_move_kernel<RR>, grid, dim3(256), 0, st, P, chains, step_base, step, \
+                       nchains);                                                              \
     break;
     GPT_CF_RANKS(CASE)
 #undef CASE

@@ -270,10 +270,11 @@ struct CfChain {
 size_t cf_lds_bytes(int r, int m, int nfeat, bool masks);
 bool cf_rank_supported(int r);
 hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
-                           int bt0, int nb, int domove, hipStream_t st);
+                           int bt0, int nb, int domove, hipStream_t st,
+                           const long long* step_base = nullptr);
 hipError_t launch_cf_gather(const CfChain* chains, int nchains, int N, hipStream_t st);
 hipError_t launch_cf_move(const CfParams& P, const CfChain* chains, int nchains, long long step,
-                          hipStream_t st);
+                          hipStream_t st, const long long* step_base = nullptr);
 hipError_t launch_cf_eval(const CfParams& P, const CfChain* chains, int nchains, int nmax,
                           int counter, hipStream_t st);
 hipError_t launch_cfg_rows(int side, int r, const double* W, const double* Oth, int rows_oth,

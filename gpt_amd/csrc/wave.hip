@@ -401,6 +401,13 @@ GPT_HD int wv_vphase_lds_dbl(int D, int r, int Q, int m) {
 
 constexpr int kWvMaxM = 64;            // minibatch rows: one per lane of the V-phase
 
+// U-noise columns per pass of the drive loop (independent Philox chains interleaved)
+#ifndef WV_NOISE_UNR
+#define WV_NOISE_UNR 4
+#endif
+#define WV_STR(x) #x
+#define WV_UNROLL(n) _Pragma(WV_STR(unroll n))
+
 // Phase stamps (gpt_sgld_session_stamps; s_memtime): dimension wave (c, k) in row c·(D+1) + k,
 // the chain's V-phase workgroup in row c·(D+1) + D.
 #define WSTAMP(row, slot)                                                                   \
@@ -810,7 +817,7 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
     constexpr int NQJ = (J + 3) / 4;
     const int NQ = unoise_nq(n);
     const uint64_t seed = Cp->seed;
-#pragma unroll 1
+    WV_UNROLL(WV_NOISE_UNR)
     for (int l = 0; l < R; ++l) {
 #pragma unroll
       for (int q = 0; q < NQJ; ++q) {

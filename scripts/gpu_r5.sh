@@ -49,6 +49,10 @@ for s in "$@"; do
     wstamps) run wstamps 200 python -u scripts/wave_stamps.py --chains 256 --steps 4 --out gpurun_out/${T}_wstamps.json ;;
     refq) run refq 300 python -u bench.py --workload kin40k_ref --no-cpu-baseline --epochs 20 ;;
     mlstamps) run mlstamps 300 python -u scripts/ml_stamps.py ;;
+    wvab) for v in product u2 u4 product; do
+            if [ $v = product ]; then L=gpt_amd/libgptsgld.so; else L=gpt_amd/libgptsgld_abl_$v.so; fi
+            run wvab_$v 200 env GPTSGLD_LIB=$L python -u scripts/wave_probe.py --chains 256 --engines wave --steps 400
+          done ;;
     *) echo "unknown step $s" ;;
   esac
 done
