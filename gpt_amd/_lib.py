@@ -65,6 +65,8 @@ SIGNATURES = {
     "gpt_sgld_timeline_slots": (C.c_int64, []),
     "gpt_debug_expm_stamps": (C.c_int, [C.c_int32, C.c_int32, P_D, C.POINTER(C.c_int64)]),
     "gpt_debug_expm": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, P_D, P_D, P_I32]),
+    "gpt_debug_gaussian_draw": (C.c_int, [C.c_int32, P_D, P_D, C.c_uint64, C.c_uint32, C.c_uint32,
+                                          C.c_uint32, P_D, P_I32]),
     "gpt_pred_trim_pool": (C.c_int, []),
     "gpt_cf_last_timing": (C.c_int, [P_D, P_D, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "gpt_cf_last_stamps": (C.c_int64, [C.POINTER(C.c_int64), C.c_int64]),

@@ -825,6 +825,27 @@ extern "C" int gpt_debug_expm(int32_t nn, int32_t count, int32_t mode, const dou
   return GPT_OK;
 }
 
+extern "C" int gpt_debug_gaussian_draw(int32_t p, const double* M, const double* x, uint64_t seed,
+                                       uint32_t c1, uint32_t c2, uint32_t c3, double* out,
+                                       int32_t* status) {
+  if (p < 1 || !M || !x || !out || !status) { set_error("bad arguments"); return GPT_ERR_BAD_DIMS; }
+  DevMem dM, dx, dz, dout, dst;
+  HIPCHK(dM.alloc(8 * (size_t)p * p));
+  HIPCHK(dx.alloc(8 * (size_t)p));
+  HIPCHK(dz.alloc(8 * (size_t)p));
+  HIPCHK(dout.alloc(8 * (size_t)p));
+  HIPCHK(dst.alloc(4));
+  HIPCHK(hipMemcpy(dM.p, M, 8 * (size_t)p * p, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dx.p, x, 8 * (size_t)p, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(dst.p, 0, 4));
+  HIPCHK(gaussian_draw_prec(dM.as<double>(), p, dx.as<double>(), seed, c1, c2, c3, dz.as<double>(),
+                            dout.as<double>(), dst.as<int32_t>(), nullptr));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, dout.p, 8 * (size_t)p, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(status, dst.p, 4, hipMemcpyDeviceToHost));
+  return GPT_OK;
+}
+
 extern "C" int gpt_debug_expm_stamps(int32_t nn, int32_t count, const double* A, int64_t* stamps) {
   if (count < 1 || !A || !stamps) { set_error("bad arguments"); return GPT_ERR_BAD_DIMS; }
   const size_t b = 8 * (size_t)nn * nn * count;

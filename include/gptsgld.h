@@ -164,6 +164,12 @@ int64_t gpt_sgld_timeline_slots(void);
  * grid engine's wave_expm; bad[c] = 1 when E_c holds a NaN (the geodesic bail-out test). */
 int gpt_debug_expm(int32_t nn, int32_t count, int32_t mode, const double* A, double* E,
                    int32_t* bad);
+/* Test entry: the Gaussian conditional draw of the Gibbs samplers (tgp.hip gaussian_draw_prec,
+ * GPT_fullw_gibbs w | U, V at 100k_movielensExperiment.jl:1092-1094, TGP.jl:61-63): M (p × p,
+ * column-major, SPD; its lower triangle is read) = L·Lᵀ, out = L⁻ᵀz + M⁻¹x with z the Philox
+ * normals (seed, c1, c2, c3) of element e = 0..p-1; *status = 1 if M is not positive definite. */
+int gpt_debug_gaussian_draw(int32_t p, const double* M, const double* x, uint64_t seed, uint32_t c1,
+                            uint32_t c2, uint32_t c3, double* out, int32_t* status);
 /* Timing of the wave engine's expm as geod calls it (three LDS slots, the first nn/2 result
  * columns), one wave per matrix: stamps[4·m + 0..3] = s_memtime at entry, after the Padé
  * polynomial, after the solve, at exit (diagnostics; scripts/expm_bench.py). */

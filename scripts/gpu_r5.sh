@@ -53,6 +53,11 @@ for s in "$@"; do
             if [ $v = product ]; then L=gpt_amd/libgptsgld.so; else L=gpt_amd/libgptsgld_abl_$v.so; fi
             run wvab_$v 200 env GPTSGLD_LIB=$L python -u scripts/wave_probe.py --chains 256 --engines wave --steps 400
           done ;;
+    chainab) for v in head new head new; do
+            if [ $v = head ]; then L=gpt_amd/libgptsgld_head.so; else L=gpt_amd/libgptsgld.so; fi
+            run chainab_$v 300 env GPTSGLD_LIB=$L python -u bench.py --no-cpu-baseline --no-single-chain --steps 1000
+          done ;;
+    chaintests) run chaintests 400 $PYT tests/test_gpu_parity.py tests/test_gpu_fullsize.py -k "chain or kin40k or powerplant or multichain or injected or nan or epoch_order or grad or trajectory" ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -219,3 +219,45 @@ def test_sideinfo_folds_equal_separate_runs(lang, stf, avg):
         for g, w_ in zip(got[f], want):
             assert g.shape == w_.shape
             assert np.array_equal(g, w_)
+
+
+@pytest.mark.parametrize("p", [1, 5, 16, 17, 100, 225, 400, 1023, 1024, 1100])
+def test_gaussian_draw_blocked_cholesky_and_solves(p):
+    """The Gibbs samplers' Gaussian conditional draw (tgp.hip gaussian_draw_prec: blocked MFMA
+    Cholesky + blocked triangular solves for p <= 1024, the column kernels past it) against numpy:
+    out = L⁻ᵀz + M⁻¹x for M = L·Lᵀ, z the Philox normals of the draw's stream.  Sizes: one panel
+    and partial panels (1, 5, 16, 17), the TGP / MovieLens sizes (100, 225 = 15², 400 = 20²), the
+    blocked limit (1023, 1024) and the fallback (1100)."""
+    import ctypes as C
+    from gpt_amd import _lib
+    from oracle import philox as px
+    rng = np.random.default_rng(p)
+    A = rng.standard_normal((p, p + 3))
+    M = np.asfortranarray(A @ A.T / p + 0.5 * np.eye(p))
+    x = rng.standard_normal(p)
+    out = np.zeros(p)
+    st = np.zeros(1, dtype=np.int32)
+    _lib.check(_lib.lib().gpt_debug_gaussian_draw(p, M.ctypes.data_as(_lib.P_D),
+                                                  x.ctypes.data_as(_lib.P_D), 11, 3, 7, 0,
+                                                  out.ctypes.data_as(_lib.P_D),
+                                                  st.ctypes.data_as(_lib.P_I32)))
+    assert st[0] == 0
+    z = px.normals(p, 11, 3, 7, 0)
+    L = np.linalg.cholesky(M)
+    want = np.linalg.solve(L.T, z) + np.linalg.solve(M, x)
+    assert np.abs(out - want).max() <= 1e-10 * np.abs(want).max(), np.abs(out - want).max()
+
+
+def test_gaussian_draw_flags_non_spd():
+    """A precision with a non-positive pivot sets the status (PosDefException in the reference)."""
+    from gpt_amd import _lib
+    p = 40
+    M = np.asfortranarray(-np.eye(p))
+    x = np.zeros(p)
+    out = np.zeros(p)
+    st = np.zeros(1, dtype=np.int32)
+    _lib.check(_lib.lib().gpt_debug_gaussian_draw(p, M.ctypes.data_as(_lib.P_D),
+                                                  x.ctypes.data_as(_lib.P_D), 1, 0, 0, 0,
+                                                  out.ctypes.data_as(_lib.P_D),
+                                                  st.ctypes.data_as(_lib.P_I32)))
+    assert st[0] == 1

@@ -335,3 +335,28 @@ def test_gmc_oracle_energy_conservation_and_w_only_rejection():
     assert u > acc[0]                                   # this epoch is rejected
     assert np.array_equal(ws[:, 0], w0)                 # w restored
     assert not np.allclose(Us[..., 0], U0)              # U keeps the proposal
+
+
+def test_kronecker_precision_from_user_statistics():
+    """The identity behind the device's w | U, V system (cf.hip cfg_wprec / cfg_wrhs, GPT_fullw_gibbs
+    :1088-1093): with Kron[i, a·r + b] = V[m_i, a]·U[u_i, b], Kronᵀ·Kron[(a,b), (a',b')] =
+    Σ_u H_u[a,a']·U[u,b]·U[u,b'] (H_u = Σ_{i∈u} V[m_i]ᵀV[m_i]) and Kronᵀ·y[(a,b)] = Σ_u h_u[a]·U[u,b]
+    (h_u = Σ_{i∈u} y_i V[m_i]), here on random ratings with users that rate nothing."""
+    rng = np.random.default_rng(5)
+    n1, n2, r, N = 30, 40, 4, 500
+    users = rng.integers(0, n1 - 3, N)
+    movies = rng.integers(0, n2, N)
+    y = rng.standard_normal(N)
+    U = rng.standard_normal((n1, r))
+    V = rng.standard_normal((n2, r))
+    K = (V[movies][:, :, None] * U[users][:, None, :]).reshape((N, r * r))
+    H = np.zeros((n1, r, r))
+    h = np.zeros((n1, r))
+    for i in range(N):
+        H[users[i]] += np.outer(V[movies[i]], V[movies[i]])
+        h[users[i]] += y[i] * V[movies[i]]
+    P = np.einsum("ub,uc->ubc", U, U)
+    Z = np.einsum("uad,ubc->abdc", H, P).reshape(r * r, r * r)     # [(a,b), (a',b')]
+    rhs = np.einsum("ua,ub->ab", h, U).reshape(r * r)
+    assert np.abs(Z - K.T @ K).max() <= 1e-12 * np.abs(K.T @ K).max()
+    assert np.abs(rhs - K.T @ y).max() <= 1e-12 * np.abs(K.T @ y).max()
