@@ -1830,16 +1830,25 @@ static int cf_sgd_run(
   DevMem d_step;
   HIPCHK(d_step.alloc(sizeof(long long)));
   g_cf_timing = CfTiming{};
+  // SGD (no Langevin noise, no Stiefel geometry) on the feature-mask path: the lazy move, one
+  // launch per epoch (cf_epoch_kernel domove = 2); GPTSGLD_CF_LAZY=0 keeps the batch-phase / move
+  // launch pairs
+  const bool lazy = !stiefel && !langevin && P.umask != nullptr &&
+                    cf_lazy_lds_bytes((int)r, (int)m, (int)(D1 + D2), rowsU + rowsV, nbatch) <=
+                        160 * 1024 &&
+                    !(std::getenv("GPTSGLD_CF_LAZY") && std::strcmp(std::getenv("GPTSGLD_CF_LAZY"), "0") == 0);
   for (int64_t epoch = 1; epoch <= burnin + maxepoch && nlive > 0; ++epoch) {
     host_randperm((int)N, seed, (int)(epoch - 1), perm.data());
     HIPCHK(hipMemcpy(d_perm.p, perm.data(), 4 * N, hipMemcpyHostToDevice));
     hipError_t e = hipSuccess;
-    if (stiefel) {
-      // the Stiefel move needs Grams over every row: the whole epoch in one workgroup per fold
+    if (stiefel || lazy) {
+      // the Stiefel move needs Grams over every row, the lazy SGD move needs none of the rows
+      // outside the batch: the whole epoch in one workgroup per fold, one launch
       HIPCHK(hipEventRecord(evs.e[0], st));
       e = launch_cf_gather(d_ch.as<CfChain>(), F, (int)N, st);
       if (e == hipSuccess)
-        e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, (epoch - 1) * nbatch, 0, nbatch, 1, st);
+        e = launch_cf_epoch(P, d_ch.as<CfChain>(), F, (epoch - 1) * nbatch, 0, nbatch,
+                            stiefel ? 1 : 2, st);
     } else if (P.stamps) {
       // the stamped first epoch: direct launches (the stamp buffer is dropped after it)
       HIPCHK(hipEventRecord(evs.e[0], st));

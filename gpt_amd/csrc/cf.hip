@@ -19,6 +19,7 @@ namespace gpt {
 
 constexpr int kCfNT = 1024;
 constexpr int kCfNW = kCfNT / 64;
+typedef double pd4 __attribute__((ext_vector_type(4)));
 
 // Diagnostic phase stamps of the epoch kernel (P.stamps, gpt_cf_last_stamps): thread 0 of chain 0
 // records s_memtime after the barrier closing each phase of the first kCfStampSteps steps.
@@ -252,14 +253,23 @@ __global__ __launch_bounds__(256) void cf_move_kernel(CfParams P, const CfChain*
   }
 }
 
+// Byte offset of the lazy move's tables (cpow, cur) in the epoch kernel's LDS: past the batch
+// carve of the masks path (w, wn, sU, sV, tU, tV, er, umk, vmk, us, ms, unx, vnx, fcnt, flist).
+GPT_HD size_t cf_lazy_offset(int r, int m, int nfeat) {
+  const size_t b = 8 * (2 * (size_t)r * r + 4 * (size_t)m * r + m) + 16 * (size_t)m +
+                   4 * (4 * (size_t)m + (size_t)nfeat) + 2 * (size_t)nfeat * m;
+  return (b + 15) / 16 * 16;
+}
+
 // domove = 0: only the batch phase of each step (sums, residuals, gradw + the w step, the
-// gradient rows); the caller launches cf_move_kernel between steps.  bt0: the launch's first
-// batch of the epoch, step0 its step.
-template <int R>
+// gradient rows); the caller launches cf_move_kernel between steps.  1: the Stiefel move in the
+// workgroup after every batch phase.  2: the lazy SGD move (below).  A template argument, so the
+// batch-phase variants are not register-allocated around the Stiefel move's arrays.  bt0: the
+// launch's first batch of the epoch, step0 its step.
+template <int R, int domove>
 __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfChain* chains,
                                                          const long long* step_base,
-                                                         long long step0, int bt0, int nb,
-                                                         int domove) {
+                                                         long long step0, int bt0, int nb) {
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const CfChain C = chains[blockIdx.x];
@@ -293,9 +303,41 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
   if (step_base) step0 += *step_base;                // graph replays: the epoch's first step
   for (int o = tid; o < R * R; o += kCfNT) w_l[o] = C.w[o];
   const double is2 = 1.0 / P.signal_var;
+  // domove = 2 (SGD, the masks path): the lazy move.  A row whose gradient is zero in a step only
+  // decays, m ← m + εU·(0 − m/σ_u²)/2 = m·c (c = 1 − εU/(2σ_u²)), so a row is stored as of the
+  // step it last moved (cur: U rows, then V rows, launch-local steps) and read as m·c^Δ (cpow,
+  // Δ = 0 … nb); the rows of a batch take the full move in the batch phase itself, the rest are
+  // brought to the launch's last step at its end.  One launch per epoch, no gradient buffers.
+  constexpr bool lazy = domove == 2;
+  const double su2 = P.sigma_u * P.sigma_u;
+  // The feature rows (users' D1, then movies' D2) stay in LDS for the launch: Fl as of their
+  // step in cur, Fc their values at the current step (formed once per step), hit the features the
+  // batch carries (their rows move this step).
+  const int nfeat = P.D1 + P.D2;
+  double* cpow = nullptr;
+  int* cur = nullptr;
+  double* Fl = nullptr;
+  double* Fc = nullptr;
+  unsigned long long* hit = nullptr;
+  if (lazy) {
+    const size_t o0 = cf_lazy_offset(R, m, nfeat);
+    cpow = (double*)(smem + o0);
+    cur = (int*)(cpow + nb + 1);
+    Fl = (double*)(smem + ((o0 + 8 * ((size_t)nb + 1) + 4 * (size_t)(P.rowsU + P.rowsV) + 15) / 16 * 16));
+    Fc = Fl + nfeat * R;
+    hit = (unsigned long long*)(Fc + nfeat * R);
+    const double lc = log1p(-P.epsU / (2 * su2));
+    for (int d = tid; d <= nb; d += kCfNT) cpow[d] = d == 0 ? 1.0 : exp((double)d * lc);
+    for (int o = tid; o < P.rowsU + P.rowsV; o += kCfNT) cur[o] = 0;
+    for (int o = tid; o < nfeat * R; o += kCfNT) {
+      const int fo = o / R, l = o - fo * R, side = fo >= P.D1 ? 1 : 0, f = fo - side * P.D1;
+      Fl[o] = gptr(side ? C.V : C.U)[(side ? P.n2 : P.n1) + f + (size_t)(side ? P.rowsV : P.rowsU) * l];
+    }
+  }
   for (int bt = bt0; bt < bt0 + nb; ++bt) {
     CF_STAMP(bt, 0);
     const long long step = step0 + (bt - bt0);
+    const int jl = bt - bt0;                           // launch-local step (lazy move)
     const int B = min(m, N - bt * m);
     const double cN = (double)N / (double)B;
     for (int ii = tid; ii < B; ii += kCfNT) {
@@ -303,6 +345,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       ms[ii] = C.ep_movie[bt * m + ii];
       er[ii] = C.ep_rating[bt * m + ii];
     }
+    if (lazy && tid < 2) hit[tid] = 0ull;
     __syncthreads();
     CF_STAMP(bt, 1);
     // per (side, ii): the feature bitmask, the first-occurrence flag and the next occurrence
@@ -310,7 +353,12 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       const int side = o >= B ? 1 : 0, ii = o - side * B;
       const int* ids = side ? ms : us;
       const int id = ids[ii];
-      if (masks) (side ? vmk : umk)[ii] = (side ? P.vmask : P.umask)[id];
+      if (masks) {
+        const uint64_t mk = (side ? P.vmask : P.umask)[id];
+        (side ? vmk : umk)[ii] = mk;
+        if (lazy) __hip_atomic_fetch_or(hit + side, (unsigned long long)mk, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       bool first = true;
       int nx = -1;
       for (int z0 = 0; z0 < B; z0 += 8) {              // eight ids read before they are compared
@@ -327,13 +375,49 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       }
       (side ? vnx : unx)[ii] = (nx + 1) | (first ? 1 << 16 : 0);
     }
+    if (lazy)                                         // the feature rows as of this step
+      for (int o = tid; o < nfeat * R; o += kCfNT) {
+        const int fo = o / R, side = fo >= P.D1 ? 1 : 0;
+        const int row = (side ? P.rowsU + P.n2 - P.D1 : P.n1) + fo;
+        Fc[o] = Fl[o] * cpow[jl - cur[row]];
+      }
     __syncthreads();
     CF_STAMP(bt, 2);
     // sumU = U[user,:] + b·sum(U[uidx,:],1), sumV likewise (:462); the feature rows in ascending
     // order (find(UserData[i,:]), the CSR order).  With the masks: four (rating, column) items
     // per thread and pass, every item's row loads issued before any sum (one memory latency per
     // pass instead of one per item)
-    if (masks) {
+    if (lazy) {
+      // the rating's own row from memory (as of this step), its feature rows from Fc, added in
+      // ascending order from 0 as the masks path below does
+      for (int o0 = tid; o0 < 2 * B * R; o0 += 4 * kCfNT) {
+        double mv[4];
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+          const int o = min(o0 + k4 * kCfNT, 2 * B * R - 1);
+          const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+          const int id = side ? ms[ii] : us[ii];
+          mv[k4] = gptr(side ? C.V : C.U)[id + (size_t)(side ? P.rowsV : P.rowsU) * l];
+        }
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+          const int o = o0 + k4 * kCfNT;
+          if (o >= 2 * B * R) break;
+          const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+          const int id = side ? ms[ii] : us[ii];
+          const double mcur = mv[k4] * cpow[jl - cur[(side ? P.rowsU : 0) + id]];
+          const double* Fs = Fc + (side ? P.D1 * R : 0) + l;
+          uint64_t mk = (side ? vmk : umk)[ii];
+          double f = 0.0;
+          while (mk) {
+            const int fb = __ffsll((long long)mk) - 1;
+            mk &= mk - 1;
+            f += Fs[fb * R];
+          }
+          (side ? sV : sU)[ii * R + l] = mcur + (side ? P.c : P.b) * f;
+        }
+      }
+    } else if (masks) {
       for (int o0 = tid; o0 < 2 * B * R; o0 += 4 * kCfNT) {
         double fv[4][4], mv[4];
         bool fh[4][4], ok[4];
@@ -393,7 +477,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         (side ? sV : sU)[ii * R + l] = gptr(M)[id + (size_t)rows * l] + (side ? P.c : P.b) * f;
       }
     }
-    if (masks)
+    if (masks && !lazy)
       for (int o = tid; o < P.D1 + P.D2; o += kCfNT) {
         const int side = o >= P.D1 ? 1 : 0, f = o - side * P.D1;
         const uint64_t* mk = side ? vmk : umk;
@@ -411,16 +495,44 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       }
     __syncthreads();
     CF_STAMP(bt, 3);
-    for (int o = tid; o < B * R; o += kCfNT) {
-      const int ii = o / R, j = o - ii * R;
-      double s1 = 0.0, s2 = 0.0;
+    // (sumU*w)[ii, :] and (sumV*w')[ii, :] on the fp64 matrix cores: one wave per (side, 16-rating
+    // tile), ⌈R/16⌉ column tiles, K = R in steps of 4 (v_mfma_f64_16x16x4f64; lane λ feeds
+    // A[λ&15][k0 + (λ>>4)] = sumX[rating][k] and B[k0 + (λ>>4)][λ&15] = w entry; rows past B and
+    // columns past R read clamped addresses and are not stored, K past R is zero)
+    {
+      constexpr int NTc = (R + 15) / 16;
+      const int lane = tid & 63, wv = tid >> 6, mts = (B + 15) / 16;
+      const int rl = lane & 15, kl = lane >> 4;
+      for (int t = wv; t < 2 * mts; t += kCfNW) {
+        const int side = t >= mts ? 1 : 0, m0 = (t - side * mts) * 16;
+        int zo = 0;                        // opaque: addresses formed per tile, not hoisted out of
+        asm volatile("" : "+v"(zo));       // the step loop into spilled registers
+        const double* S = (side ? sV : sU) + zo;
+        const double* wz = w_l + zo;
+        const int arow = min(m0 + rl, B - 1);
+        pd4 acc[NTc];
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        s1 = fma(sU[ii * R + i], w_l[i + R * j], s1);      // (sumU*w)[j]
-        s2 = fma(sV[ii * R + i], w_l[j + R * i], s2);      // (sumV*w')[j]
+        for (int nt = 0; nt < NTc; ++nt) acc[nt] = pd4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k0 = 0; k0 < R; k0 += 4) {
+          const int k = k0 + kl, kc = min(k, R - 1);
+          const double a = k < R ? S[arow * R + kc] : 0.0;
+#pragma unroll
+          for (int nt = 0; nt < NTc; ++nt) {
+            const int n = min(nt * 16 + rl, R - 1);
+            const double bv = side ? wz[n + R * kc] : wz[kc + R * n];
+            acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[nt], 0, 0, 0);
+          }
+        }
+        double* Tt = side ? tV : tU;
+#pragma unroll
+        for (int nt = 0; nt < NTc; ++nt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = m0 + kl + 4 * q, col = nt * 16 + rl;
+            if (row < B && col < R) Tt[row * R + col] = acc[nt][q];
+          }
       }
-      tU[ii * R + j] = s1;
-      tV[ii * R + j] = s2;
     }
     __syncthreads();
     CF_STAMP(bt, 4);
@@ -434,24 +546,44 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     CF_STAMP(bt, 5);
     // gradw (:466, :473-477) and the w step of :479-483 into wn
     // (GPT_fixw / GPT_fixw_sideinfo, :56-156 / :282-404: w is fixed — no gradw, no step)
-    for (int o = tid; o < R * R; o += kCfNT) {
-      if (P.fixw) { wn_l[o] = w_l[o]; continue; }
-      const int i = o % R, j = o / R;
-      double g = 0.0;
-      int ii = 0;
-      for (; ii + 4 <= B; ii += 4) {                   // four ratings' reads in flight, summed in order
-        double t4[4];
+    // gradw[i, j] = Σ_ii sumU[ii, i]·(er_ii·sumV[ii, j]) on the fp64 matrix cores: one wave per
+    // 16 × 16 tile of w, K = the batch's ratings in steps of 4 (past B: zero); then the w step of
+    // :479-483 per entry.  (The round-4 form summed er·(sumU·sumV)·is2 rating by rating per entry:
+    // the same sum, rounded differently.)
+    if (!P.fixw) {
+      constexpr int NTw = (R + 15) / 16;
+      const int lane = tid & 63, wv = tid >> 6, rl = lane & 15, kl = lane >> 4;
+      for (int t = wv; t < NTw * NTw; t += kCfNW) {
+        const int it = t / NTw, jt = t - it * NTw;
+        const int ia = min(it * 16 + rl, R - 1), jb = min(jt * 16 + rl, R - 1);
+        int zo = 0;                        // (as above)
+        asm volatile("" : "+v"(zo));
+        const double* sUz = sU + zo;
+        const double* sVz = sV + zo;
+        const double* erz = er + zo;
+        pd4 acc = pd4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int k0 = 0; k0 < B; k0 += 4) {
+          const int k = k0 + kl, kc = min(k, B - 1);
+          const double a = k < B ? sUz[kc * R + ia] : 0.0;
+          const double bv = erz[kc] * sVz[kc * R + jb];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
+        }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) t4[u] = er[ii + u] * (sU[(ii + u) * R + i] * sV[(ii + u) * R + j]) * is2;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) g += t4[u];
+        for (int q = 0; q < 4; ++q) {
+          const int i = it * 16 + kl + 4 * q, j = jt * 16 + rl;
+          if (i < R && j < R) {
+            const int ow = i + R * j;
+            const double G = acc[q] * is2 * cN - w_l[ow] / (P.sigma_w * P.sigma_w);
+            double wn = w_l[ow] + P.epsw * G / 2;
+            if (P.langevin)
+              wn = wn + sqrt(P.epsw) * normal_at(P.seed, (uint32_t)ow, (uint32_t)step, kCfWNoise, 0);
+            wn_l[ow] = wn;
+          }
+        }
       }
-      for (; ii < B; ++ii) g += er[ii] * (sU[ii * R + i] * sV[ii * R + j]) * is2;
-      const double G = g * cN - w_l[o] / (P.sigma_w * P.sigma_w);
-      double wn = w_l[o] + P.epsw * G / 2;
-      if (P.langevin)
-        wn = wn + sqrt(P.epsw) * normal_at(P.seed, (uint32_t)o, (uint32_t)step, kCfWNoise, 0);
-      wn_l[o] = wn;
+    } else {
+      for (int o = tid; o < R * R; o += kCfNT) wn_l[o] = w_l[o];
     }
     // gradient rows in rating order (:467-471): the first rating of a user / movie in the batch
     // sums its row; feature rows sum over the ratings whose user / movie carries them
@@ -464,10 +596,53 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       const double* T = side ? tU : tV;     // Vtemp = e·(sumU*w), Utemp = e·(sumV*w')
       double g = 0.0;
       for (int z = ii; z >= 0; z = (nxl[z] & 0xFFFF) - 1) g += P.a * (er[z] * T[z * R + l]) * is2;
-      double* G = side ? C.GV : C.GU;
-      gptr_w(G)[id + (size_t)(side ? P.rowsV : P.rowsU) * l] = g * cN;
+      const size_t e = id + (size_t)(side ? P.rowsV : P.rowsU) * l;
+      if (lazy) {                                     // the row's move of this step (cf_move)
+        double* M = side ? C.V : C.U;
+        const double m0 = gptr(M)[e] * cpow[jl - cur[(side ? P.rowsU : 0) + id]];
+        gptr_w(M)[e] = m0 + P.epsU * (g * cN - m0 / su2) / 2;
+      } else {
+        gptr_w(side ? C.GV : C.GU)[e] = g * cN;
+      }
     }
-    for (int o = tid; o < (P.D1 + P.D2) * R; o += kCfNT) {
+    if (lazy) {
+      // feature rows: G[f, l] = Σ_ii [f ∈ mask_ii]·er_ii·T[ii, l] on the fp64 matrix cores (one
+      // wave per 16 features × 16 columns of a side, K = the ratings; A = the mask bit as 0 / 1),
+      // then the move of every feature the batch carries, in LDS (Fl)
+      constexpr int LT = (R + 15) / 16;
+      const int lane = tid & 63, wv = tid >> 6, rl = lane & 15, kl = lane >> 4;
+      const int FT1 = (P.D1 + 15) / 16, FT2 = (P.D2 + 15) / 16;
+      for (int t = wv; t < (FT1 + FT2) * LT; t += kCfNW) {
+        const int ft = t / LT, lt = t - ft * LT, side = ft >= FT1 ? 1 : 0;
+        const int f0 = (ft - side * FT1) * 16, Ds = side ? P.D2 : P.D1;
+        int zo = 0;
+        asm volatile("" : "+v"(zo));
+        const uint64_t* mk = (side ? vmk : umk) + zo;
+        const double* T = (side ? tU : tV) + zo;
+        const double* erz = er + zo;
+        const int fa = f0 + rl, lb = min(lt * 16 + rl, R - 1);
+        pd4 acc = pd4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int k0 = 0; k0 < B; k0 += 4) {
+          const int k = k0 + kl, kc = min(k, B - 1);
+          const double a = (k < B && ((mk[kc] >> fa) & 1ull)) ? 1.0 : 0.0;
+          const double bv = erz[kc] * T[kc * R + lb];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
+        }
+        const double ab = P.a * (side ? P.c : P.b);
+        const unsigned long long hs = hit[side];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int f = f0 + kl + 4 * q, l = lt * 16 + rl;
+          if (f < Ds && l < R && ((hs >> f) & 1ull)) {
+            const int o = ((side ? P.D1 : 0) + f) * R + l;
+            const double g = ab * acc[q] * is2, m0 = Fc[o];
+            Fl[o] = m0 + P.epsU * (g * cN - m0 / su2) / 2;
+          }
+        }
+      }
+    }
+    for (int o = tid; o < (lazy ? 0 : (P.D1 + P.D2) * R); o += kCfNT) {
       const int side = o >= P.D1 * R ? 1 : 0;
       const int x = side ? o - P.D1 * R : o, f = x / R, l = x - f * R;
       const int* ids = side ? ms : us;
@@ -510,7 +685,17 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     }
     __syncthreads();
     CF_STAMP(bt, 6);
-    if (domove && (!cf_move<R>(P, C.U, C.GU, P.rowsU, 0, step, scr) ||
+    if (lazy) {                                       // the moved rows are current as of jl + 1
+      for (int o = tid; o < 2 * B; o += kCfNT) {
+        const int side = o >= B ? 1 : 0, ii = o - side * B;
+        if ((side ? vnx : unx)[ii] >> 16) cur[(side ? P.rowsU : 0) + (side ? ms : us)[ii]] = jl + 1;
+      }
+      for (int o = tid; o < P.D1 + P.D2; o += kCfNT) {
+        const int side = o >= P.D1 ? 1 : 0, f = o - side * P.D1;
+        if ((hit[side] >> f) & 1ull) cur[(side ? P.rowsU + P.n2 : P.n1) + f] = jl + 1;
+      }
+    }
+    if (domove == 1 && (!cf_move<R>(P, C.U, C.GU, P.rowsU, 0, step, scr) ||
                    !cf_move<R>(P, C.V, C.GV, P.rowsV, 1, step, scr))) {
       if (tid == 0) __hip_atomic_store(C.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
@@ -518,6 +703,18 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     CF_STAMP(bt, 7);
     for (int o = tid; o < R * R; o += kCfNT) w_l[o] = wn_l[o];
     __syncthreads();
+  }
+  if (lazy) {                                         // every row brought to the launch's end
+    const int nUe = P.rowsU * R;
+    for (int o = tid; o < nUe + P.rowsV * R; o += kCfNT) {
+      const int side = o >= nUe ? 1 : 0, x = o - side * nUe;
+      const int rows = side ? P.rowsV : P.rowsU, l = x / rows, row = x - l * rows;
+      const int d = nb - cur[(side ? P.rowsU : 0) + row];
+      double* M = side ? C.V : C.U;
+      const int base = side ? P.n2 : P.n1;
+      if (row >= base) gptr_w(M)[x] = Fl[((side ? P.D1 : 0) + row - base) * R + l] * cpow[d];
+      else if (d > 0) gptr_w(M)[x] = gptr(M)[x] * cpow[d];
+    }
   }
   for (int o = tid; o < R * R; o += kCfNT) C.w[o] = w_l[o];
 }
@@ -941,6 +1138,13 @@ size_t cf_lds_bytes(int r, int m, int nfeat, bool masks) {
 }
 
 
+// LDS of the lazy-move epoch launch (domove = 2): the batch carve, then cpow[0..nb], cur[rows],
+// the feature rows Fl, Fc (nfeat × r each) and the two hit masks
+size_t cf_lazy_lds_bytes(int r, int m, int nfeat, int rows, int nb) {
+  return al16(cf_lazy_offset(r, m, nfeat) + 8 * ((size_t)nb + 1) + 4 * (size_t)rows) +
+         16 * (size_t)nfeat * r + 16 + 16;
+}
+
 bool cf_rank_supported(int r) {
   switch (r) {
 #define CASE(RR) case RR:
@@ -951,24 +1155,36 @@ bool cf_rank_supported(int r) {
   }
 }
 
+template <int RR, int DM>
+static hipError_t launch_cf_epoch_t(const CfParams& P, const CfChain* chains, int nchains,
+                                    long long step0, int bt0, int nb, size_t lds, hipStream_t st,
+                                    const long long* step_base) {
+  static std::atomic<uint64_t> attr{0};
+  hipError_t e = set_max_lds_once((const void*)cf_epoch_kernel<RR, DM>, 160 * 1024, attr);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((cf_epoch_kernel<RR, DM>), dim3(nchains), dim3(kCfNT), lds, st, P, chains,
+                     step_base, step0, bt0, nb);
+  return hipGetLastError();
+}
+
 hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
                            int bt0, int nb, int domove, hipStream_t st,
                            const long long* step_base) {
-  const size_t lds = cf_lds_bytes(P.r, P.m, P.D1 + P.D2, P.D1 <= 64 && P.D2 <= 64);
+  size_t lds = cf_lds_bytes(P.r, P.m, P.D1 + P.D2, P.D1 <= 64 && P.D2 <= 64);
+  if (domove == 2)
+    lds = std::max(lds, cf_lazy_lds_bytes(P.r, P.m, P.D1 + P.D2, P.rowsU + P.rowsV, nb));
   switch (P.r) {
 #define CASE(RR)                                                                              \
-  case RR: {                                                                                  \
-    static std::atomic<uint64_t> attr{0};                                                     \
-    hipError_t e = set_max_lds_once((const void*)cf_epoch_kernel<RR>, 160 * 1024, attr);      \
-    if (e != hipSuccess) return e;                                                            \
-    hipLaunchKernelGGL(cf_epoch_kernel<RR>, dim3(nchains), dim3(kCfNT), lds, st, P, chains,   \
-                       step_base, step0, bt0, nb, domove);                                    \
-  } break;
+  case RR:                                                                                    \
+    if (domove == 1)                                                                          \
+      return launch_cf_epoch_t<RR, 1>(P, chains, nchains, step0, bt0, nb, lds, st, step_base); \
+    if (domove == 2)                                                                          \
+      return launch_cf_epoch_t<RR, 2>(P, chains, nchains, step0, bt0, nb, lds, st, step_base); \
+    return launch_cf_epoch_t<RR, 0>(P, chains, nchains, step0, bt0, nb, lds, st, step_base);
     GPT_CF_RANKS(CASE)
 #undef CASE
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 // The training ratings of every fold in this epoch's order, once per epoch (the batch kernels

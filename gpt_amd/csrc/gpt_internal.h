@@ -268,6 +268,7 @@ struct CfChain {
 };
 
 size_t cf_lds_bytes(int r, int m, int nfeat, bool masks);
+size_t cf_lazy_lds_bytes(int r, int m, int nfeat, int rows, int nb);
 bool cf_rank_supported(int r);
 hipError_t launch_cf_epoch(const CfParams& P, const CfChain* chains, int nchains, long long step0,
                            int bt0, int nb, int domove, hipStream_t st,

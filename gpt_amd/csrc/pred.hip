@@ -416,6 +416,94 @@ __global__ __launch_bounds__(64 * kRowsWaves) void pred_vphase_rows_kernel(
   }
 }
 
+// The rows V-phase as a persistent loop over (sample, 64-row) tiles: every workgroup (one per CU,
+// the tile's D·R rows take ~80 KB of LDS at r = 20) loads the NEXT tile's rows into registers
+// (up to 16 per lane and wave) while its waves run the current tile's core entries from LDS, so the
+// tile's HBM read overlaps the LDS work instead of alternating with it.  DD > 0: D as a
+// compile-time constant, so a core entry's D offsets are one scalar load and its D LDS reads are
+// issued together (with a runtime D each factor waited for its offset's scalar load and then its
+// LDS read, one after the other: 4.2 ms of a 10.9 ms call at r = 20).  The core-entry loop and the
+// partial sums are the rows kernel's (the same doubles).
+constexpr int kRowsPfMax = 16;
+template <int DD>
+__global__ __launch_bounds__(64 * kRowsWaves) void pred_vphase_rows_pf_kernel(
+    const double* __restrict__ w, const double* __restrict__ T, const int32_t* __restrict__ offs,
+    int Drt, int R, long long Ntest, int Q, double* __restrict__ fhat, int S) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int D = DD > 0 ? DD : Drt;
+  double* tl = (double*)smem;                       // [k·R + l][64]
+  double* part = tl + (size_t)D * R * 64;           // [wave][64]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int DR = D * R;
+  const long long nti = (Ntest + 63) / 64, ntiles = nti * S;
+  double nx[kRowsPfMax];
+  auto fetch = [&](long long tile) {
+    const int s = (int)(tile / nti);
+    const long long i0 = (tile - (long long)s * nti) * 64, i = i0 + lane;
+    const double* Ts = T + (size_t)s * DR * Ntest + (i < Ntest ? i : i0);
+#pragma unroll
+    for (int x = 0; x < kRowsPfMax; ++x) {
+      const int row = wv + kRowsWaves * x;
+      if (row < DR) nx[x] = gptr(Ts)[(size_t)row * Ntest];
+    }
+  };
+  auto park = [&]() {
+#pragma unroll
+    for (int x = 0; x < kRowsPfMax; ++x) {
+      const int row = wv + kRowsWaves * x;
+      if (row < DR) tl[row * 64 + lane] = nx[x];
+    }
+  };
+  const auto* ofq = cptr(offs);
+  const int qa = Q * wv / kRowsWaves, qb = Q * (wv + 1) / kRowsWaves;
+  long long tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  fetch(tile);
+  park();
+  __syncthreads();
+  for (; tile < ntiles; tile += gridDim.x) {
+    const long long tnext = tile + gridDim.x;
+    if (tnext < ntiles) fetch(tnext);                // in flight under the core entries below
+    const int s = (int)(tile / nti);
+    const long long i = (tile - (long long)s * nti) * 64 + lane;
+    const auto* wq = cptr(w + (size_t)s * Q);
+    double f0 = 0.0, f1 = 0.0;
+    int q = qa;
+    for (; q + 2 <= qb; q += 2) {
+      double v0 = wq[q], v1 = wq[q + 1];
+      if constexpr (DD > 0) {
+        int o0[DD], o1[DD];
+#pragma unroll
+        for (int k = 0; k < DD; ++k) { o0[k] = ofq[q * DD + k]; o1[k] = ofq[(q + 1) * DD + k]; }
+#pragma unroll
+        for (int k = 0; k < DD; ++k) { v0 *= tl[o0[k] + lane]; v1 *= tl[o1[k] + lane]; }
+      } else {
+        for (int k = 0; k < D; ++k) {
+          v0 *= tl[ofq[q * D + k] + lane];
+          v1 *= tl[ofq[(q + 1) * D + k] + lane];
+        }
+      }
+      f0 += v0;
+      f1 += v1;
+    }
+    if (q < qb) {
+      double v0 = wq[q];
+      for (int k = 0; k < D; ++k) v0 *= tl[ofq[q * D + k] + lane];
+      f0 += v0;
+    }
+    part[wv * 64 + lane] = f0 + f1;
+    __syncthreads();                                 // every wave is done with tl and part
+    if (wv == 0) {
+      double f = part[lane];
+#pragma unroll
+      for (int x = 1; x < kRowsWaves; ++x) f += part[x * 64 + lane];
+      if (i < Ntest) fhat[(size_t)s * Ntest + i] = f;
+    }
+    if (tnext < ntiles) park();
+    __syncthreads();
+  }
+}
+
 // V-phase with pair tables: the D factors of V[q, i] are taken two dimensions at a time from
 // per-test-row tables PP_t[a·r + b] = temp[2t, a]·temp[2t+1, b] (an odd last dimension keeps its r
 // rows), built once per (sample, 64 rows) workgroup, so a core entry costs ⌈D/2⌉ lane-contiguous LDS
@@ -572,6 +660,53 @@ static hipError_t vphase_pairs(int NTp, const double* w, const double* T, const 
   }
 }
 
+// The rows V-phase: the persistent prefetching kernel while a tile's D·R rows fit 16 per wave
+// (GPTSGLD_PRED_ROWS_PF=0: the one-tile-per-workgroup kernel, for comparison), as many workgroups
+// as the LDS lets every CU hold.
+template <int DD>
+static hipError_t launch_rows_pf(const double* w, const double* T, const int32_t* offs, int D, int r,
+                                 long long Ntest, int Q, double* fhat, int Sc, size_t rlds,
+                                 hipStream_t st) {
+  static std::atomic<uint64_t> attr{0};
+  hipError_t e = set_max_lds_once((const void*)pred_vphase_rows_pf_kernel<DD>, 160 * 1024, attr);
+  if (e != hipSuccess) return e;
+  int dev = 0, cus = 0;
+  e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  const long long per_cu = std::max<long long>(1, (long long)(160 * 1024) / (long long)rlds);
+  const long long ntiles = (Ntest + 63) / 64 * (long long)Sc;
+  const unsigned grid = (unsigned)std::min<long long>(ntiles, per_cu * cus);
+  hipLaunchKernelGGL(pred_vphase_rows_pf_kernel<DD>, dim3(grid), dim3(64 * kRowsWaves), rlds, st, w,
+                     T, offs, D, r, Ntest, Q, fhat, Sc);
+  return hipGetLastError();
+}
+
+static hipError_t launch_vphase_rows(const double* w, const double* T, const int32_t* offs, int D,
+                                     int r, long long Ntest, int Q, double* fhat, int Sc,
+                                     size_t rlds, hipStream_t st) {
+  static const bool pf = [] {
+    const char* ev = std::getenv("GPTSGLD_PRED_ROWS_PF");
+    return !(ev && std::strcmp(ev, "0") == 0);
+  }();
+  if (pf && D * r <= kRowsWaves * kRowsPfMax) {
+    switch (D) {
+#define DCASE(X) case X: return launch_rows_pf<X>(w, T, offs, D, r, Ntest, Q, fhat, Sc, rlds, st);
+      DCASE(2) DCASE(3) DCASE(4) DCASE(5) DCASE(6) DCASE(7) DCASE(8) DCASE(9) DCASE(10) DCASE(12)
+#undef DCASE
+      default: return launch_rows_pf<0>(w, T, offs, D, r, Ntest, Q, fhat, Sc, rlds, st);
+    }
+  }
+  if (rlds > 64 * 1024) {
+    static std::atomic<uint64_t> attr{0};
+    const hipError_t e = set_max_lds_once((const void*)pred_vphase_rows_kernel, 160 * 1024, attr);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(pred_vphase_rows_kernel, dim3((unsigned)((Ntest + 63) / 64), Sc),
+                     dim3(64 * kRowsWaves), rlds, st, w, T, offs, D, r, Ntest, Q, fhat);
+  return hipGetLastError();
+}
+
 // The prediction's pass buffers come from a private stream-ordered pool per device that keeps its
 // memory between calls (release threshold ∞: the default threshold 0 unmapped and remapped the
 // ~GBs of every call, ≈0.45 ms of a 7 ms call) without changing the device's default pool for the
@@ -697,14 +832,8 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
       continue;
     }
     if (!tile_vphase) {
-      if (rlds > 64 * 1024) {
-        static std::atomic<uint64_t> attr{0};
-        e = set_max_lds_once((const void*)pred_vphase_rows_kernel, 160 * 1024, attr);
-        if (e != hipSuccess) break;
-      }
-      hipLaunchKernelGGL(pred_vphase_rows_kernel, vg, dim3(64 * kRowsWaves), rlds, st, w + (size_t)s0 * Q, T,
-                         offs, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest);
-      e = hipGetLastError();
+      e = launch_vphase_rows(w + (size_t)s0 * Q, T, offs, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest,
+                             Sc, rlds, st);
       if (timing && e == hipSuccess) {
         (void)hipEventRecord(ev[2], st);
         (void)hipEventSynchronize(ev[2]);

@@ -19,6 +19,10 @@ run() {   # run NAME SECONDS CMD...
   return 0
 }
 RP="rocprofv3 --kernel-trace --stats --output-format csv"
+squeeze() {   # gzip the kernel traces of a profile directory (gpurun merges back at most 64 MiB)
+  for f in "gpurun_out/${T}_prof_$1"/*kernel_trace.csv; do [ -f "$f" ] && gzip -f "$f"; done
+  return 0
+}
 for s in "$@"; do
   case $s in
     tests)   run tests 400 $PYT tests ;;
@@ -26,17 +30,19 @@ for s in "$@"; do
     repro0)  run repro0 300 env GPTSGLD_MAX_INFLIGHT=0 $RP -d gpurun_out/${T}_prof_repro0 -o repro -- python -u scripts/refprof_repro.py --maps gpurun_out/${T}_repro0_maps.txt ;;
     repro8)  run repro8 300 $RP -d gpurun_out/${T}_prof_repro8 -o repro -- python -u scripts/refprof_repro.py --maps gpurun_out/${T}_repro8_maps.txt ;;
     bench)   run bench 300 python -u bench.py ;;
-    prof)    run prof 600 $RP -d gpurun_out/${T}_prof_bench -o bench -- python -u bench.py --no-cpu-baseline ;;
+    prof)    run prof 600 $RP -d gpurun_out/${T}_prof_bench -o bench -- python -u bench.py --no-cpu-baseline; squeeze bench ;;
     sweep500) run sweep500 600 python -u scripts/kin40k_step_sweep.py --n 500 --r 5 --epsw 5e-6,1e-5,1.2e-5,1e-4 --epsU 1e-8,3e-8,1e-7,3e-7 --out gpurun_out/${T}_sweep500.json ;;
     sweep150) run sweep150 600 python -u scripts/kin40k_step_sweep.py --n 150 --r 5 --epsw 5e-6,1e-5,3e-5,1e-4 --epsU 1e-8,3e-8,1e-7,3e-7 --out gpurun_out/${T}_sweep150.json ;;
     sweep150r20) run sweep150r20 600 python -u scripts/kin40k_step_sweep.py --n 150 --r 20 --epsw 1e-5,3e-5,1e-4,2e-4 --epsU 1e-8,3e-8,1e-7,3e-7 --out gpurun_out/${T}_sweep150r20.json ;;
     ref)     run ref 600 python -u bench.py --workload kin40k_ref ;;
-    refprof) run refprof 600 $RP -d gpurun_out/${T}_prof_ref -o ref -- python -u bench.py --workload kin40k_ref --no-cpu-baseline ;;
+    refprof) run refprof 600 $RP -d gpurun_out/${T}_prof_ref -o ref -- python -u bench.py --workload kin40k_ref --no-cpu-baseline; squeeze ref ;;
     ml)      run ml 300 python -u bench.py --workload movielens ;;
-    mlprof)  run mlprof 600 $RP -d gpurun_out/${T}_prof_ml -o ml -- python -u bench.py --workload movielens --no-cpu-baseline ;;
+    mlprof)  run mlprof 600 $RP -d gpurun_out/${T}_prof_ml -o ml -- python -u bench.py --workload movielens --no-cpu-baseline; squeeze ml ;;
     pp)      run pp 300 python -u bench.py --workload powerplant ;;
     quality) run quality 900 $PYT tests/test_gpu_quality.py tests/test_gpu_fullsize.py ;;
-    gibbsprof) run gibbsprof 300 $RP -d gpurun_out/${T}_prof_gibbs -o gibbs -- python -u scripts/time_gibbs.py --sweeps 40 ;;
+    gibbsprof) run gibbsprof 300 $RP -d gpurun_out/${T}_prof_gibbs -o gibbs -- python -u scripts/time_gibbs.py --sweeps 40; squeeze gibbs ;;
+    ppprof) run ppprof 600 $RP -d gpurun_out/${T}_prof_pp -o pp -- python -u bench.py --workload powerplant --no-cpu-baseline; squeeze pp ;;
+    predclk) run predclk 200 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --kernel-trace --output-format csv -d gpurun_out/${T}_prof_predclk -o predclk -- python -u scripts/time_pred.py --S 256 --tiles 44 --vphases pairs ;;
     pair) run pair 300 python -u bench.py --epsw 1e-4 --epsU 1e-8 --no-cpu-baseline --no-single-chain ;;
     hq) run hq 300 $PYT tests/test_gpu_quality.py -k "bench_shape or powerplant_config2_converged" ;;
     mltests) run mltests 400 $PYT tests/test_gpu_movielens.py tests/test_gpu_tgp.py tests/test_gpu_quality.py -k "movielens or tgp or gibbs or bench_shape" ;;
@@ -49,6 +55,8 @@ for s in "$@"; do
     wstamps) run wstamps 200 python -u scripts/wave_stamps.py --chains 256 --steps 4 --out gpurun_out/${T}_wstamps.json ;;
     refq) run refq 300 python -u bench.py --workload kin40k_ref --no-cpu-baseline --epochs 20 ;;
     mlstamps) run mlstamps 300 python -u scripts/ml_stamps.py ;;
+    mlstamps0) run mlstamps0 300 env GPTSGLD_CF_LAZY=0 python -u scripts/ml_stamps.py ;;
+    mlab) for v in 0 1 0 1; do run mlab_$v 300 env GPTSGLD_CF_LAZY=$v python -u bench.py --workload movielens --no-cpu-baseline; done ;;
     wvab) for v in product u2 u4 product; do
             if [ $v = product ]; then L=gpt_amd/libgptsgld.so; else L=gpt_amd/libgptsgld_abl_$v.so; fi
             run wvab_$v 200 env GPTSGLD_LIB=$L python -u scripts/wave_probe.py --chains 256 --engines wave --steps 400
@@ -58,6 +66,11 @@ for s in "$@"; do
             run chainab_$v 300 env GPTSGLD_LIB=$L python -u bench.py --no-cpu-baseline --no-single-chain --steps 1000
           done ;;
     chaintests) run chaintests 400 $PYT tests/test_gpu_parity.py tests/test_gpu_fullsize.py -k "chain or kin40k or powerplant or multichain or injected or nan or epoch_order or grad or trajectory" ;;
+    predab) for v in head new head new; do
+              if [ $v = head ]; then L=gpt_amd/libgptsgld_head.so; else L=gpt_amd/libgptsgld.so; fi
+              run predab5_$v 200 env GPTSGLD_LIB=$L python -u scripts/time_pred.py --S 256 --tiles 44 --vphases pairs --reps 5
+              run predab20_$v 200 env GPTSGLD_LIB=$L python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 5
+            done ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -9,6 +9,7 @@ bench's hipEvent pair measures) and (b) the kernels' summed durations, per kerne
     python scripts/prof_timed.py TRACE.csv --steps 20 [--bench LINE.json] [--out OUT.json]
 """
 import argparse
+import gzip
 import csv
 import json
 import sys
@@ -22,7 +23,8 @@ def main():
     ap.add_argument("--bench", default=None, help="the bench's JSON line, to compare against")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
-    rows = list(csv.DictReader(open(args.trace)))
+    opener = gzip.open if args.trace.endswith(".gz") else open
+    rows = list(csv.DictReader(opener(args.trace, "rt")))
     for r in rows:
         r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     rows.sort(key=lambda r: r["s"])
