@@ -340,6 +340,33 @@ def movielens_bytes_per_step(ud, md, m, r):
     return gather + grads + move
 
 
+def movielens_lazy_bytes_per_step(ud, md, m, r, nb):
+    """HBM bytes per minibatch step of the lazy SGD path (cf_epoch_kernel domove = 2, one launch per
+    epoch): the batch's triples and both feature masks, the batch's U / V rows read (the feature
+    rows live in LDS for the launch), the touched rows' move (read + write), and the per-epoch
+    flush of every row (read + write) and the feature rows' load / store, spread over the epoch's
+    nb steps."""
+    n1, D1 = ud.shape
+    n2, D2 = md.shape
+    gather = m * (4 + 4 + 8 + 8 + 8) + 8 * m * r * 2
+    moved = 2 * 8 * r * 2 * m
+    epoch = 2 * 8 * r * (n1 + D1 + n2 + D2) + 2 * 8 * r * (D1 + D2)
+    return gather + moved + epoch / nb
+
+
+def gibbs_flops_per_sweep(N, n1, n2, r):
+    """fp64 flops of one GPT_fullw_gibbs sweep as cf.hip / tgp.hip run it: the user / movie
+    conditionals (per rating the X row, 2r^2, and the precision update, 2r^2; per row an r x r
+    Cholesky and two solves), the w | U, V statistics (2r^2 per rating), the precision GEMM
+    Z = H^T P (2 p^2 n1, p = r^2), the right-hand side (2 p n1), the p x p Cholesky (p^3 / 3 FMAs)
+    and three triangular solves (p^2 each)."""
+    p = r * r
+    rows = 2 * N * 4 * r * r + (n1 + n2) * (2 * r ** 3 / 3 + 4 * r * r)
+    stats = 2 * N * r * r
+    wsys = 2 * p * p * n1 + 2 * p * n1 + 2 * p ** 3 / 3 + 3 * 2 * p * p
+    return rows + stats + wsys
+
+
 def movielens_cpu_baseline(fold1, w0, cfg, epochs=1):
     """The numpy restatement of GPT_fullw_sideinfo (oracle/movielens_ref.py, 1 core) on fold 1
     for ``epochs`` epochs of the live configuration."""
@@ -409,7 +436,10 @@ def movielens_main(args):
     steps_all = gather_over_ranks(float(tm["fold_steps"]), dev)
     value = sum(steps_all) / dt
     mins = [float(o[5].min()) for o in outs]
-    bstep = movielens_bytes_per_step(ud, md, cfg["m"], r)
+    nbat = -(-trs[0].shape[0] // cfg["m"])
+    bdense = movielens_bytes_per_step(ud, md, cfg["m"], r)
+    lazy = tm.get("mode", 0) == 2
+    bstep = movielens_lazy_bytes_per_step(ud, md, cfg["m"], r, nbat) if lazy else bdense
     ep_us = 1e3 * tm["epoch_ms"] / max(tm["epochs"], 1)
     steps_per_launch = tm["fold_steps"] / max(tm["epochs"], 1)
     achieved = bstep * steps_per_launch / (ep_us * 1e-6) / 1e9
@@ -434,10 +464,21 @@ def movielens_main(args):
         gibbs = {"sampler": "GPT_fullw_gibbs (100k_movielensExperiment.jl:1032-1129), fold 1, r=%d" % r,
                  "sweeps": 15 + gsweeps, "seconds": dtg, "sweeps_per_s": (15 + gsweeps) / dtg,
                  "ms_per_sweep": 1e3 * dtg / (15 + gsweeps),
+                 "roofline": {"bound": "mfma", "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                              "flops_per_sweep": gibbs_flops_per_sweep(tr1.shape[0], ud1.shape[0],
+                                                                       md1.shape[0], r),
+                              "kernel": "whole sweep (chol_blk_kernel, cfg_rows_kernel x 3, "
+                                        "cfg_wprec_kernel, trsv_blk_kernel x 3, ...)",
+                              "note": "latency-bound: the 400 x 400 Cholesky's 25 serial panels "
+                                      "are 0.50 of 1.35 ms of kernels per sweep "
+                                      "(profiles/r5r_gibbs_kernel_stats.csv)"},
                  "test_rmse_running_avg_final": float(curve[-1]),
                  "test_rmse_running_avg_min": float(curve.min()),
                  "reference_fullWresults_h5_r15": {"at_same_sweep": float(refg[min(gsweeps, len(refg)) - 1]),
                                                     "final_1000": float(refg[-1]), "min": float(refg.min())}}
+        gr = gibbs["roofline"]
+        gr["achieved"] = gr["flops_per_sweep"] / (1e-3 * gibbs["ms_per_sweep"]) / 1e12
+        gr["frac"] = gr["achieved"] / gr["peak"]
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = movielens_cpu_baseline(folds[0], w0, cfg)
@@ -460,12 +501,21 @@ def movielens_main(args):
                        "parallelism": "folds%dx%d" % (len(folds), world)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "cf_gather_kernel + %d x (cf_epoch_kernel<%d> batch phase + "
-                                   "cf_move_kernel<%d>)" % (nb, r, r),
+                         "kernel": ("cf_gather_kernel + cf_epoch_kernel<%d, lazy move> (one launch "
+                                    "per epoch: %d minibatch steps per fold workgroup)" % (r, nb))
+                                   if lazy else
+                                   ("cf_gather_kernel + %d x (cf_epoch_kernel<%d> batch phase + "
+                                    "cf_move_kernel<%d>)" % (nb, r, r)),
                          "kernel_us": ep_us, "kernel_us_note": "per epoch of every live fold's %d "
-                         "minibatch steps (one batch-phase launch, one workgroup per fold, and one "
-                         "row-parallel move launch per step), hipEvents inside "
-                         "gpt_cf_fullw_sideinfo_folds around the epoch's launches" % nb,
+                         "minibatch steps, hipEvents inside gpt_cf_fullw_sideinfo_folds around the "
+                         "epoch's launches (%s)" % (nb, "one epoch launch, one workgroup per fold, "
+                         "the lazy SGD move: rows outside a batch only decay and are read as m*c^k"
+                         if lazy else "one batch-phase launch, one workgroup per fold, and one "
+                         "row-parallel move launch per step"),
+                         "launch_mode": int(tm.get("mode", 0)),
+                         "survey_8d_bytes_per_step": bdense,
+                         "survey_8d_note": "the reference's dense per-step move of every U / V row "
+                                           "(read M, G; write M, G) priced in",
                          "eval_kernel_us": 1e3 * tm["eval_ms"] / max(tm["epochs"], 1),
                          "algorithmic_bytes_per_step": bstep,
                          "algorithmic_bytes_per_launch": bstep * steps_per_launch,

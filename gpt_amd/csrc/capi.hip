@@ -1658,6 +1658,7 @@ struct CfFold {
 // epoch / eval launch, read after the per-epoch status copy that synchronises anyway.
 struct CfTiming { double epoch_ms, eval_ms; int64_t epochs, evals, fold_steps; };
 static thread_local CfTiming g_cf_timing{};
+static thread_local int32_t g_cf_mode = 0;      // gpt_cf_last_mode
 // GPTSGLD_CF_STAMPS=1: per-phase s_memtime of fold 0's first epoch (gpt_cf_last_stamps)
 static thread_local std::vector<long long> g_cf_stamps;
 
@@ -1837,6 +1838,7 @@ static int cf_sgd_run(
                     cf_lazy_lds_bytes((int)r, (int)m, (int)(D1 + D2), rowsU + rowsV, nbatch) <=
                         160 * 1024 &&
                     !(std::getenv("GPTSGLD_CF_LAZY") && std::strcmp(std::getenv("GPTSGLD_CF_LAZY"), "0") == 0);
+  g_cf_mode = stiefel ? 1 : (lazy ? 2 : 0);
   for (int64_t epoch = 1; epoch <= burnin + maxepoch && nlive > 0; ++epoch) {
     host_randperm((int)N, seed, (int)(epoch - 1), perm.data());
     HIPCHK(hipMemcpy(d_perm.p, perm.data(), 4 * N, hipMemcpyHostToDevice));
@@ -2024,6 +2026,12 @@ extern "C" int gpt_cf_last_timing(double* epoch_ms, double* eval_ms, int64_t* ep
   *eval_ms = g_cf_timing.eval_ms;
   *epochs = g_cf_timing.epochs;
   *fold_steps = g_cf_timing.fold_steps;
+  return GPT_OK;
+}
+
+extern "C" int gpt_cf_last_mode(int32_t* mode) {
+  if (!mode) { set_error("gpt_cf_last_mode: null output"); return GPT_ERR_BAD_DIMS; }
+  *mode = g_cf_mode;
   return GPT_OK;
 }
 

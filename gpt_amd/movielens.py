@@ -214,11 +214,16 @@ def GPT_fixw_gibbs(Rating, UserData, MovieData, Ratingtest, signal_var, sigma_u,
 
 def last_timing():
     """Device time of the last CF SGD / SGLD call on this thread (gpt_cf_last_timing): dict with
-    epoch_ms (cf_epoch_kernel launches), eval_ms (cf_eval_kernel), epochs and fold_steps."""
+    epoch_ms (cf_epoch_kernel launches), eval_ms (cf_eval_kernel), epochs, fold_steps and mode
+    (gpt_cf_last_mode: 0 batch-phase + move launches per step, 1 Stiefel epoch launch, 2 lazy SGD
+    epoch launch)."""
     em, vm = C.c_double(), C.c_double()
     ne, fs = C.c_int64(), C.c_int64()
     check(lib().gpt_cf_last_timing(C.byref(em), C.byref(vm), C.byref(ne), C.byref(fs)))
-    return dict(epoch_ms=em.value, eval_ms=vm.value, epochs=ne.value, fold_steps=fs.value)
+    mode = C.c_int32()
+    check(lib().gpt_cf_last_mode(C.byref(mode)))
+    return dict(epoch_ms=em.value, eval_ms=vm.value, epochs=ne.value, fold_steps=fs.value,
+                mode=mode.value)
 
 
 def GPT_fullw_sideinfo_folds(Ratings, UserData, MovieData, Ratingtests, signal_var, sigma_u,

@@ -320,6 +320,12 @@ int gpt_cf_fullw_sideinfo_folds(int64_t F, const double* const* Rating, const in
  * launches, fold_steps = minibatch steps summed over the folds live in each launch.  No
  * reference counterpart (measurement, bench.py --workload movielens). */
 int gpt_cf_last_timing(double* epoch_ms, double* eval_ms, int64_t* epochs, int64_t* fold_steps);
+/* How the last CF SGD / SGLD call on this thread launched its epochs: 0 = per minibatch a
+ * batch-phase launch (one workgroup per fold) and a row-parallel move launch; 1 = one launch per
+ * epoch with the Stiefel move inside (stiefel = 1); 2 = one launch per epoch with the lazy SGD
+ * move (langevin = stiefel = 0 on the feature-mask path: rows outside a batch only decay, read as
+ * m·c^Δ).  No reference counterpart (measurement). */
+int gpt_cf_last_mode(int32_t* mode);
 /* With GPTSGLD_CF_STAMPS set, the last CF SGD call recorded s_memtime at the 8 phase boundaries
  * of fold 0's first 64 steps of its first epoch (batch load, masks / links, sums, sum·w,
  * residuals, gradients, U / V moves): copies up to cap of them (64 x 8, step-major) and returns
