@@ -501,7 +501,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     // columns past R read clamped addresses and are not stored, K past R is zero)
     {
       constexpr int NTc = (R + 15) / 16;
-      const int lane = tid & 63, wv = tid >> 6, mts = (B + 15) / 16;
+      const int lane = tid & 63, wv = uni(tid >> 6), mts = (B + 15) / 16;
       const int rl = lane & 15, kl = lane >> 4;
       for (int t = wv; t < 2 * mts; t += kCfNW) {
         const int side = t >= mts ? 1 : 0, m0 = (t - side * mts) * 16;
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     // the same sum, rounded differently.)
     if (!P.fixw) {
       constexpr int NTw = (R + 15) / 16;
-      const int lane = tid & 63, wv = tid >> 6, rl = lane & 15, kl = lane >> 4;
+      const int lane = tid & 63, wv = uni(tid >> 6), rl = lane & 15, kl = lane >> 4;
       for (int t = wv; t < NTw * NTw; t += kCfNW) {
         const int it = t / NTw, jt = t - it * NTw;
         const int ia = min(it * 16 + rl, R - 1), jb = min(jt * 16 + rl, R - 1);
@@ -610,7 +610,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       // wave per 16 features × 16 columns of a side, K = the ratings; A = the mask bit as 0 / 1),
       // then the move of every feature the batch carries, in LDS (Fl)
       constexpr int LT = (R + 15) / 16;
-      const int lane = tid & 63, wv = tid >> 6, rl = lane & 15, kl = lane >> 4;
+      const int lane = tid & 63, wv = uni(tid >> 6), rl = lane & 15, kl = lane >> 4;
       const int FT1 = (P.D1 + 15) / 16, FT2 = (P.D2 + 15) / 16;
       for (int t = wv; t < (FT1 + FT2) * LT; t += kCfNW) {
         const int ft = t / LT, lt = t - ft * LT, side = ft >= FT1 ? 1 : 0;

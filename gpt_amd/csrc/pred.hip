@@ -199,7 +199,8 @@ __global__ __launch_bounds__(kNT) void mean_sse_kernel(const double* __restrict_
 // ---- stacked-sample prediction on the fp64 matrix cores (GPT_SGLD.jl:233-243 over S samples)
 //
 // phidotU of S samples at once is one GEMM per dimension k:
-//   T[(s·D + k)·R + l][i] = Σ_j U_s[j, l, k] · phi[j, k, i]     (M = S·R, N = Ntest, K = n)
+//   T[s][i/64][k·R + l][i%64] = Σ_j U_s[j, l, k] · phi[j, k, i]     (M = S·R, N = Ntest, K = n)
+// (tile-contiguous: the V-phase reads a (sample, 64 rows) tile's D·R rows as one block)
 // run on v_mfma_f64_16x16x4f64, then the V-phase (computeV / computefhat) per (sample, 64-row tile)
 // reads its R·D temp rows.  Both operands are K(j)-contiguous; lane λ feeds the K pair
 // j0 + 2(λ>>4) + {0,1} of row/column λ&15 as one 16-B load and the two halves go to two MFMAs
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __res
                                                              int n, int D, int R,
                                                              long long Ntest, int S,
                                                              double* __restrict__ T,
-                                                             long long ldT) {
+                                                             long long nti64) {
   constexpr int WC = 32 * TM, WI = 32 * TN;        // workgroup tile (2 × 2 waves of 16TM × 16TN)
   const int SR = S * R;
   const int nct = (SR + WC - 1) / WC;
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __res
   const long long rest = logical / nct;
   const long long it = rest % nit;
   const int k = (int)(rest / nit);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, kl = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6), kl = lane >> 4;
   const int cw = ct * WC + (wv & 1) * 16 * TM;
   const long long iw = it * WI + (wv >> 1) * 16 * TN;
   const __attribute__((address_space(1))) double* pa[TM];
@@ -321,7 +322,8 @@ __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __res
         const long long i = iw + 16 * u + (lane & 15);
         if (c < SR && i < Ntest) {
           const int sm = c / R, l = c - sm * R;
-          gptr_w(T)[(((size_t)sm * D + k) * R + l) * (size_t)ldT + i] = acc[t][u][reg];
+          gptr_w(T)[((((size_t)sm * nti64 + (size_t)(i >> 6)) * D + k) * R + l) * 64 + (i & 63)] =
+              acc[t][u][reg];
         }
       }
 }
@@ -345,10 +347,10 @@ __global__ __launch_bounds__(kNT) void pred_vphase_kernel(const double* __restri
   const int Bt = (int)min((long long)64, Ntest - i0);
   for (int x = tid; x < Q * D; x += kNT) I_l[x] = I0[x];
   for (int q = tid; q < Q; q += kNT) w_l[q] = w[(size_t)s * Q + q];
-  const double* Ts = T + (size_t)s * D * R * Ntest + i0;
+  const double* Ts = T + ((size_t)s * ((Ntest + 63) / 64) + blockIdx.x) * D * R * 64;
   for (int x = tid; x < D * R * 64; x += kNT) {
     const int row = x >> 6, i = x & 63;
-    if (i < Bt) temp_l[row * MP + i] = gptr(Ts)[(size_t)row * Ntest + i];
+    if (i < Bt) temp_l[row * MP + i] = gptr(Ts)[(size_t)row * 64 + i];
   }
   __syncthreads();
   vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, I_l, w_l, Q, D, 0, Bt, [&](int comp, int i, double v) {
@@ -379,13 +381,13 @@ __global__ __launch_bounds__(64 * kRowsWaves) void pred_vphase_rows_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* tl = (double*)smem;                       // [k·R + l][64]
   double* part = tl + (size_t)D * R * 64;           // [wave][64]
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   const int s = blockIdx.y;
   const long long i0 = (long long)blockIdx.x * 64;
   const long long i = i0 + lane;
   const bool ok = i < Ntest;
-  const double* Ts = T + (size_t)s * D * R * Ntest + (ok ? i : i0);
-  for (int row = wv; row < D * R; row += kRowsWaves) tl[row * 64 + lane] = gptr(Ts)[(size_t)row * Ntest];
+  const double* Ts = T + ((size_t)s * ((Ntest + 63) / 64) + blockIdx.x) * D * R * 64 + lane;
+  for (int row = wv; row < D * R; row += kRowsWaves) tl[row * 64 + lane] = gptr(Ts)[(size_t)row * 64];
   __syncthreads();
   const auto* ofq = cptr(offs);
   const auto* wq = cptr(w + (size_t)s * Q);
@@ -417,56 +419,74 @@ __global__ __launch_bounds__(64 * kRowsWaves) void pred_vphase_rows_kernel(
 }
 
 // The rows V-phase as a persistent loop over (sample, 64-row) tiles: every workgroup (one per CU,
-// the tile's D·R rows take ~80 KB of LDS at r = 20) loads the NEXT tile's rows into registers
-// (up to 16 per lane and wave) while its waves run the current tile's core entries from LDS, so the
-// tile's HBM read overlaps the LDS work instead of alternating with it.  DD > 0: D as a
+// the tile's D·R rows take ~80 KB of LDS at r = 20) keeps the rows of its next two tiles in
+// flight in registers (up to 16 per lane and wave each) while its waves run the current tile's
+// core entries from LDS, so the tiles' HBM reads overlap the LDS work instead of alternating with
+// it (one tile ahead behind __syncthreads, which waits for them: 3.7 ms per 224-sample call).  DD > 0: D as a
 // compile-time constant, so a core entry's D offsets are one scalar load and its D LDS reads are
 // issued together (with a runtime D each factor waited for its offset's scalar load and then its
 // LDS read, one after the other: 4.2 ms of a 10.9 ms call at r = 20).  The core-entry loop and the
 // partial sums are the rows kernel's (the same doubles).
-constexpr int kRowsPfMax = 16;
-template <int DD>
-__global__ __launch_bounds__(64 * kRowsWaves) void pred_vphase_rows_pf_kernel(
+// NW waves per workgroup, NPW prefetched rows per wave.  16 waves (the launch uses 16) measured
+// 3.48 ms per 224-sample r = 20 call against 5.06 ms with 8 waves whose core-entry loop keeps each
+// pair's 2·D LDS reads in flight together (`profiles/r5ah_rows_vphase_waves.txt`): the tile
+// stream needs the memory parallelism of 16 waves more than the loop needs the registers.
+template <int DD, int NW, int NPW>
+__global__ __launch_bounds__(64 * NW) void pred_vphase_rows_pf_kernel(
     const double* __restrict__ w, const double* __restrict__ T, const int32_t* __restrict__ offs,
     int Drt, int R, long long Ntest, int Q, double* __restrict__ fhat, int S) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int D = DD > 0 ? DD : Drt;
   double* tl = (double*)smem;                       // [k·R + l][64]
   double* part = tl + (size_t)D * R * 64;           // [wave][64]
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // the core entries' offsets (Q·D, the same for every tile) and the tile's sample's w (Q) in
+  // LDS: the entry loop reads them as wave-uniform LDS broadcasts, in order with its data reads
+  // (as scalar loads each pair waited for its offsets — the lgkm counter is shared — and the w
+  // lines of every new sample missed the scalar cache)
+  int* ofl = (int*)(part + NW * 64);
+  double* wl = (double*)(ofl + ((Q * (DD > 0 ? DD : Drt) + 3) & ~3));
+  const int lane = threadIdx.x & 63, wv = uni(threadIdx.x >> 6);
   const int DR = D * R;
+  for (int x = threadIdx.x; x < Q * D; x += 64 * NW) ofl[x] = offs[x];
   const long long nti = (Ntest + 63) / 64, ntiles = nti * S;
-  double nx[kRowsPfMax];
-  auto fetch = [&](long long tile) {
+  // two register buffers: the rows of tile t + 2G are loaded while tile t runs and tile t + G
+  // waits in the other buffer; the barriers inside the loop wait for LDS only (s_barrier after
+  // lgkmcnt(0)), so these loads stay in flight across them (__syncthreads would wait for them)
+  double nxa[NPW + 1], nxb[NPW + 1];                // + the sample's w entry of this thread
+  const bool wreg = Q <= 64 * NW;                    // w rides with the rows (else loaded at park)
+  auto fetch = [&](long long tile, double (&nx)[NPW + 1]) {
     const int s = (int)(tile / nti);
+    if (wreg) nx[NPW] = w[(size_t)s * Q + min((int)threadIdx.x, Q - 1)];
     const long long i0 = (tile - (long long)s * nti) * 64, i = i0 + lane;
-    const double* Ts = T + (size_t)s * DR * Ntest + (i < Ntest ? i : i0);
+    const double* Ts = T + (size_t)tile * DR * 64 + lane;    // the tile's rows: one block
 #pragma unroll
-    for (int x = 0; x < kRowsPfMax; ++x) {
-      const int row = wv + kRowsWaves * x;
-      if (row < DR) nx[x] = gptr(Ts)[(size_t)row * Ntest];
+    for (int x = 0; x < NPW; ++x) {
+      const int row = wv + NW * x;
+      if (row < DR) nx[x] = gptr(Ts)[(size_t)row * 64];
     }
   };
-  auto park = [&]() {
+  auto park = [&](const double (&nx)[NPW + 1], long long tile) {
 #pragma unroll
-    for (int x = 0; x < kRowsPfMax; ++x) {
-      const int row = wv + kRowsWaves * x;
+    for (int x = 0; x < NPW; ++x) {
+      const int row = wv + NW * x;
       if (row < DR) tl[row * 64 + lane] = nx[x];
     }
+    if (wreg) {
+      if ((int)threadIdx.x < Q) wl[threadIdx.x] = nx[NPW];
+    } else {
+      for (int x = threadIdx.x; x < Q; x += 64 * NW) wl[x] = w[(size_t)(tile / nti) * Q + x];
+    }
   };
-  const auto* ofq = cptr(offs);
-  const int qa = Q * wv / kRowsWaves, qb = Q * (wv + 1) / kRowsWaves;
-  long long tile = blockIdx.x;
-  if (tile >= ntiles) return;
-  fetch(tile);
-  park();
-  __syncthreads();
-  for (; tile < ntiles; tile += gridDim.x) {
-    const long long tnext = tile + gridDim.x;
-    if (tnext < ntiles) fetch(tnext);                // in flight under the core entries below
+  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  const int* ofq = ofl;
+  const int qa = Q * wv / NW, qb = Q * (wv + 1) / NW;
+  const long long G = gridDim.x;
+  // tile t from LDS; loads of t + 2G into ld; t + G (in pk) parked at the end
+  auto body = [&](long long tile, double (&ld)[NPW + 1], const double (&pk)[NPW + 1]) {
+    if (tile + 2 * G < ntiles) fetch(tile + 2 * G, ld);
     const int s = (int)(tile / nti);
     const long long i = (tile - (long long)s * nti) * 64 + lane;
-    const auto* wq = cptr(w + (size_t)s * Q);
+    const double* wq = wl;
     double f0 = 0.0, f1 = 0.0;
     int q = qa;
     for (; q + 2 <= qb; q += 2) {
@@ -475,8 +495,11 @@ __global__ __launch_bounds__(64 * kRowsWaves) void pred_vphase_rows_pf_kernel(
         int o0[DD], o1[DD];
 #pragma unroll
         for (int k = 0; k < DD; ++k) { o0[k] = ofq[q * DD + k]; o1[k] = ofq[(q + 1) * DD + k]; }
+        double t0[DD], t1[DD];
 #pragma unroll
-        for (int k = 0; k < DD; ++k) { v0 *= tl[o0[k] + lane]; v1 *= tl[o1[k] + lane]; }
+        for (int k = 0; k < DD; ++k) { t0[k] = tl[o0[k] + lane]; t1[k] = tl[o1[k] + lane]; }
+#pragma unroll
+        for (int k = 0; k < DD; ++k) { v0 *= t0[k]; v1 *= t1[k]; }
       } else {
         for (int k = 0; k < D; ++k) {
           v0 *= tl[ofq[q * D + k] + lane];
@@ -492,15 +515,29 @@ __global__ __launch_bounds__(64 * kRowsWaves) void pred_vphase_rows_pf_kernel(
       f0 += v0;
     }
     part[wv * 64 + lane] = f0 + f1;
-    __syncthreads();                                 // every wave is done with tl and part
+    lds_barrier();                                   // every wave is done with tl and part
     if (wv == 0) {
       double f = part[lane];
 #pragma unroll
-      for (int x = 1; x < kRowsWaves; ++x) f += part[x * 64 + lane];
+      for (int x = 1; x < NW; ++x) f += part[x * 64 + lane];
       if (i < Ntest) fhat[(size_t)s * Ntest + i] = f;
     }
-    if (tnext < ntiles) park();
-    __syncthreads();
+    if (tile + G < ntiles) park(pk, tile + G);
+    lds_barrier();
+  };
+  long long tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  fetch(tile, nxa);
+  if (tile + G < ntiles) fetch(tile + G, nxb);
+  park(nxa, tile);
+  __syncthreads();
+  for (;;) {
+    body(tile, nxa, nxb);
+    tile += G;
+    if (tile >= ntiles) break;
+    body(tile, nxb, nxa);
+    tile += G;
+    if (tile >= ntiles) break;
   }
 }
 
@@ -534,8 +571,7 @@ __global__ void pred_pair_offs_kernel(const int32_t* __restrict__ I0, int Q, int
 template <int NT>
 __global__ __launch_bounds__(64 * kPairWaves) void pred_vphase_pairs_kernel(
     const double* __restrict__ w, const double* __restrict__ T, const int32_t* __restrict__ offp,
-    int D, int R, long long Ntest, int Q, double* __restrict__ fhat, long long ldT,
-    long long ldF) {
+    int D, int R, long long Ntest, int Q, double* __restrict__ fhat, long long ldF) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* pp = (double*)smem;                                   // [row][64]
   const int tid = threadIdx.x, lane = tid & 63, wv = uni(tid >> 6);
@@ -543,7 +579,7 @@ __global__ __launch_bounds__(64 * kPairWaves) void pred_vphase_pairs_kernel(
   const long long i0 = (long long)blockIdx.x * 64;
   const long long i = i0 + lane;
   const bool ok = i < Ntest;
-  const double* Ts = T + (size_t)s * D * R * ldT + (ok ? i : i0);
+  const double* Ts = T + ((size_t)s * ((Ntest + 63) / 64) + blockIdx.x) * D * R * 64 + lane;
   const int rows = (D / 2) * R * R + (D & 1) * R;
   double* red = pp + (size_t)rows * 64;
   // tables: wave w builds tables w, w + 4, ..; the 2·R temp rows of a table (512 contiguous
@@ -553,8 +589,8 @@ __global__ __launch_bounds__(64 * kPairWaves) void pred_vphase_pairs_kernel(
     const bool two = 2 * t + 1 < D;
 #pragma unroll
     for (int x = 0; x < 5; ++x) {
-      a[x] = x < R ? gptr(Ts)[(size_t)((2 * t) * R + x) * ldT] : 0.0;
-      b[x] = (x < R && two) ? gptr(Ts)[(size_t)((2 * t + 1) * R + x) * ldT] : 1.0;
+      a[x] = x < R ? gptr(Ts)[(size_t)((2 * t) * R + x) * 64] : 0.0;
+      b[x] = (x < R && two) ? gptr(Ts)[(size_t)((2 * t + 1) * R + x) * 64] : 1.0;
     }
     double* dst = pp + (size_t)t * R * R * 64 + lane;
     if (two) {
@@ -611,49 +647,49 @@ static size_t pred_vphase_lds_bytes(int D, int r, int Q) {
 template <int TM, int TN>
 static void launch_pred_gemm_t(const double* Us, const double* phitest, int n, int D, int r,
                                long long Ntest, int Sc, double* T, hipStream_t st,
-                               long long ldT) {
+                               long long nti64) {
   const long long total = (long long)((Sc * r + 32 * TM - 1) / (32 * TM)) *
                           ((Ntest + 32 * TN - 1) / (32 * TN)) * D;
   const unsigned grid = (unsigned)((total + kXcds - 1) / kXcds * kXcds);
   if ((n & 1) == 0)
     hipLaunchKernelGGL((pred_temp_mfma_kernel<true, TM, TN>), dim3(grid), dim3(256), 0, st, Us,
-                       phitest, n, D, r, Ntest, Sc, T, ldT);
+                       phitest, n, D, r, Ntest, Sc, T, nti64);
   else
     hipLaunchKernelGGL((pred_temp_mfma_kernel<false, TM, TN>), dim3(grid), dim3(256), 0, st, Us,
-                       phitest, n, D, r, Ntest, Sc, T, ldT);
+                       phitest, n, D, r, Ntest, Sc, T, nti64);
 }
 
 static hipError_t launch_pred_gemm(const double* Us, const double* phitest, int n, int D, int r,
                                    long long Ntest, int Sc, double* T, hipStream_t st,
-                                   long long ldT = -1) {
-  if (ldT < 0) ldT = Ntest;
+                                   long long nti64 = -1) {
+  if (nti64 < 0) nti64 = (Ntest + 63) / 64;
   const char* ev = std::getenv("GPTSGLD_PRED_TILE");
   const int tile = ev ? std::atoi(ev) : 44;
-  if (tile == 22) launch_pred_gemm_t<2, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st, ldT);
-  else if (tile == 42) launch_pred_gemm_t<4, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st, ldT);
-  else if (tile == 24) launch_pred_gemm_t<2, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st, ldT);
-  else launch_pred_gemm_t<4, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st, ldT);
+  if (tile == 22) launch_pred_gemm_t<2, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st, nti64);
+  else if (tile == 42) launch_pred_gemm_t<4, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st, nti64);
+  else if (tile == 24) launch_pred_gemm_t<2, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st, nti64);
+  else launch_pred_gemm_t<4, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st, nti64);
   return hipGetLastError();
 }
 
 template <int NN>
 static hipError_t launch_vphase_pairs(const double* w, const double* T, const int32_t* offp, int D,
                                       int r, long long rows, int Q, double* fhat, int Sc,
-                                      long long ldT, long long ldF, size_t plds, hipStream_t st) {
+                                      long long ldF, size_t plds, hipStream_t st) {
   static std::atomic<uint64_t> attr{0};
   hipError_t e = set_max_lds_once((const void*)pred_vphase_pairs_kernel<NN>, 160 * 1024, attr);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pred_vphase_pairs_kernel<NN>, dim3((unsigned)((rows + 63) / 64), Sc),
-                     dim3(64 * kPairWaves), plds, st, w, T, offp, D, r, rows, Q, fhat, ldT, ldF);
+                     dim3(64 * kPairWaves), plds, st, w, T, offp, D, r, rows, Q, fhat, ldF);
   return hipGetLastError();
 }
 
 static hipError_t vphase_pairs(int NTp, const double* w, const double* T, const int32_t* offp,
                                int D, int r, long long rows, int Q, double* fhat, int Sc,
-                               long long ldT, long long ldF, size_t plds, hipStream_t st) {
+                               long long ldF, size_t plds, hipStream_t st) {
   switch (NTp) {
 #define PCASE(NN) \
-    case NN: return launch_vphase_pairs<NN>(w, T, offp, D, r, rows, Q, fhat, Sc, ldT, ldF, plds, st);
+    case NN: return launch_vphase_pairs<NN>(w, T, offp, D, r, rows, Q, fhat, Sc, ldF, plds, st);
     PCASE(1) PCASE(2) PCASE(3) PCASE(4) PCASE(5) PCASE(6) PCASE(7) PCASE(8)
 #undef PCASE
     default: return hipErrorInvalidValue;
@@ -663,22 +699,25 @@ static hipError_t vphase_pairs(int NTp, const double* w, const double* T, const 
 // The rows V-phase: the persistent prefetching kernel while a tile's D·R rows fit 16 per wave
 // (GPTSGLD_PRED_ROWS_PF=0: the one-tile-per-workgroup kernel, for comparison), as many workgroups
 // as the LDS lets every CU hold.
-template <int DD>
+constexpr int kRowsPfWaves = 16;
+template <int DD, int NPW, int NW = kRowsPfWaves>
 static hipError_t launch_rows_pf(const double* w, const double* T, const int32_t* offs, int D, int r,
-                                 long long Ntest, int Q, double* fhat, int Sc, size_t rlds,
-                                 hipStream_t st) {
+                                 long long Ntest, int Q, double* fhat, int Sc, hipStream_t st) {
   static std::atomic<uint64_t> attr{0};
-  hipError_t e = set_max_lds_once((const void*)pred_vphase_rows_pf_kernel<DD>, 160 * 1024, attr);
+  hipError_t e =
+      set_max_lds_once((const void*)pred_vphase_rows_pf_kernel<DD, NW, NPW>, 160 * 1024, attr);
   if (e != hipSuccess) return e;
   int dev = 0, cus = 0;
   e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
-  const long long per_cu = std::max<long long>(1, (long long)(160 * 1024) / (long long)rlds);
+  const size_t lds = 8 * (size_t)D * r * 64 + 8 * (size_t)NW * 64 + 4 * (((size_t)Q * D + 3) & ~3) +
+                     8 * (size_t)Q;
+  const long long per_cu = std::max<long long>(1, (long long)(160 * 1024) / (long long)lds);
   const long long ntiles = (Ntest + 63) / 64 * (long long)Sc;
   const unsigned grid = (unsigned)std::min<long long>(ntiles, per_cu * cus);
-  hipLaunchKernelGGL(pred_vphase_rows_pf_kernel<DD>, dim3(grid), dim3(64 * kRowsWaves), rlds, st, w,
-                     T, offs, D, r, Ntest, Q, fhat, Sc);
+  hipLaunchKernelGGL((pred_vphase_rows_pf_kernel<DD, NW, NPW>), dim3(grid), dim3(64 * NW), lds, st,
+                     w, T, offs, D, r, Ntest, Q, fhat, Sc);
   return hipGetLastError();
 }
 
@@ -689,13 +728,17 @@ static hipError_t launch_vphase_rows(const double* w, const double* T, const int
     const char* ev = std::getenv("GPTSGLD_PRED_ROWS_PF");
     return !(ev && std::strcmp(ev, "0") == 0);
   }();
-  if (pf && D * r <= kRowsWaves * kRowsPfMax) {
-    switch (D) {
-#define DCASE(X) case X: return launch_rows_pf<X>(w, T, offs, D, r, Ntest, Q, fhat, Sc, rlds, st);
-      DCASE(2) DCASE(3) DCASE(4) DCASE(5) DCASE(6) DCASE(7) DCASE(8) DCASE(9) DCASE(10) DCASE(12)
+  if (pf && D * r <= kRowsPfWaves * 16) {
+    // rows per wave: 10 (D·r ≤ 160: kin40kExperiment.jl's D = 8, r = 20) or 16
+    if (D * r <= kRowsPfWaves * 10) {
+      switch (D) {
+#define DCASE(X) case X: return launch_rows_pf<X, 10>(w, T, offs, D, r, Ntest, Q, fhat, Sc, st);
+        DCASE(2) DCASE(3) DCASE(4) DCASE(5) DCASE(6) DCASE(7) DCASE(8) DCASE(9) DCASE(10) DCASE(12)
 #undef DCASE
-      default: return launch_rows_pf<0>(w, T, offs, D, r, Ntest, Q, fhat, Sc, rlds, st);
+        default: return launch_rows_pf<0, 10>(w, T, offs, D, r, Ntest, Q, fhat, Sc, st);
+      }
     }
+    return launch_rows_pf<0, 16>(w, T, offs, D, r, Ntest, Q, fhat, Sc, st);
   }
   if (rlds > 64 * 1024) {
     static std::atomic<uint64_t> attr{0};
@@ -761,7 +804,10 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     }
   // temp of up to ~8 GiB of samples per pass; a pass of several workgroup tiles takes a multiple of
   // 128 / gcd(128, r) samples, so its S·r columns fill whole 128-column tiles (no MFMA padding)
-  const size_t per_sample = 8 * (size_t)D * r * (size_t)Ntest;
+  // T per sample: (Ntest / 64 tiles) × (D·r rows) × 64 doubles, tile-contiguous, so a V-phase
+  // tile's rows are one block (row-major [D·r][Ntest] made each tile 160 strided 512-B reads at
+  // r = 20: 1.9 TB/s, 4.1 ms of the 224-sample call with no arithmetic at all)
+  const size_t per_sample = 8 * (size_t)D * r * (size_t)((Ntest + 63) / 64 * 64);
   int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)S, ((size_t)8 << 30) / per_sample));
   int unit = 1;
   {
@@ -770,6 +816,12 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     unit = 128 / g;
     if (chunk < S && chunk >= unit) chunk = chunk / unit * unit;
   }
+  // GPTSGLD_PRED_ALLOC=plain: hipMalloc / hipFree around the call instead of the private pool
+  // (diagnostic: page-size / TLB behaviour of the pass buffer)
+  static const bool plain_alloc = [] {
+    const char* ev = std::getenv("GPTSGLD_PRED_ALLOC");
+    return ev && std::strcmp(ev, "plain") == 0;
+  }();
   hipMemPool_t pool = nullptr;
   hipError_t e = pred_pool(&pool);
   if (e != hipSuccess) return e;
@@ -778,8 +830,13 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
   size_t tbytes = 0;
   for (;;) {          // out of device memory: halve the pass (whole 128-column tiles while it can)
     tbytes = (per_sample * chunk + 255) / 256 * 256;
-    e = hipMallocFromPoolAsync((void**)&T, tbytes + 4 * (size_t)Q * D + 4 * (size_t)Q * NTp, pool,
-                               st);
+    if (plain_alloc) {
+      e = hipStreamSynchronize(st);
+      if (e == hipSuccess) e = hipMalloc((void**)&T, tbytes + 4 * (size_t)Q * D + 4 * (size_t)Q * NTp);
+    } else {
+      e = hipMallocFromPoolAsync((void**)&T, tbytes + 4 * (size_t)Q * D + 4 * (size_t)Q * NTp, pool,
+                                 st);
+    }
     if (e != hipErrorOutOfMemory || chunk == 1) break;
     (void)hipGetLastError();
     chunk = chunk / 2 >= unit ? chunk / 2 / unit * unit : std::max(1, chunk / 2);
@@ -819,7 +876,7 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
     if (pairs) {
       e = vphase_pairs(NTp, w + (size_t)s0 * Q, T, offp, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest,
-                       Sc, Ntest, Ntest, plds, st);
+                       Sc, Ntest, plds, st);
       if (timing && e == hipSuccess) {
         (void)hipEventRecord(ev[2], st);
         (void)hipEventSynchronize(ev[2]);
@@ -860,7 +917,13 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
       default: e = hipErrorInvalidValue;
     }
   }
-  hipError_t ef = hipFreeAsync(T, st);
+  hipError_t ef = hipSuccess;
+  if (plain_alloc) {
+    ef = hipStreamSynchronize(st);
+    if (ef == hipSuccess) ef = hipFree(T);
+  } else {
+    ef = hipFreeAsync(T, st);
+  }
   return e != hipSuccess ? e : ef;
 }
 

@@ -71,6 +71,14 @@ for s in "$@"; do
               run predab5_$v 200 env GPTSGLD_LIB=$L python -u scripts/time_pred.py --S 256 --tiles 44 --vphases pairs --reps 5
               run predab20_$v 200 env GPTSGLD_LIB=$L python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 5
             done ;;
+    pred20prof) run pred20prof 200 $RP -d gpurun_out/${T}_prof_pred20 -o p20 -- python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 3 ;;
+    pred20pmc) run pred20pmc 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_LDS SQ_INSTS_SMEM --kernel-trace --output-format csv -d gpurun_out/${T}_prof_p20pmc -o p20pmc -- python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 1 &&
+               run pred20pmc2 120 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/${T}_prof_p20pmc2 -o p20pmc2 -- python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 1 ;;
+    scstamps) run scstamps 200 python -u scripts/phase_stamps.py --chains 1 --steps 30 ;;
+    gridsync) run gridsync 120 ./diagbin/gridsync_bench ;;
+    rowsabl) for a in 0 1 2 0; do run rowsabl_$a 200 env GPTSGLD_ROWS_ABL=$a $RP -d gpurun_out/${T}_prof_rabl$a -o r -- python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 3; done ;;
+    allocab) for a in pool plain pool plain; do run allocab_$a 200 env GPTSGLD_PRED_ALLOC=$a $RP -d gpurun_out/${T}_prof_alloc_$a -o r -- python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 3; done ;;
+    nwab) for a in 8 16 8 16; do run nwab_$a 200 env GPTSGLD_PRED_ROWS_NW=$a $RP -d gpurun_out/${T}_prof_nw$a -o r -- python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 3; done ;;
     *) echo "unknown step $s" ;;
   esac
 done
