@@ -367,22 +367,39 @@ def gibbs_flops_per_sweep(N, n1, n2, r):
     return rows + stats + wsys
 
 
-def movielens_cpu_baseline(fold1, w0, cfg, epochs=1):
-    """The numpy restatement of GPT_fullw_sideinfo (oracle/movielens_ref.py, 1 core) on fold 1
-    for ``epochs`` epochs of the live configuration."""
+def movielens_cpu_baseline(folds, w0, cfg, epochs=12):
+    """The C++ fp64 restatement of GPT_fullw_sideinfo's SGD epochs (oracle/cpu/movielens_cpu.cpp,
+    the reference's dense per-step move of every row; checked against oracle/movielens_ref.py by
+    tests/test_oracle.py) on the same 5 folds, one OpenMP thread per fold, ``epochs`` epochs from
+    the same starting state, each epoch's train / test evaluation included; plus one fold on one
+    core for the per-core rate."""
+    from oracle import cpu_lib
     from oracle import movielens_ref as M
-    tr, te, ud, md, mu, sd = fold1
-    t0 = time.perf_counter()
-    M.GPT_fullw_sideinfo(tr, ud, md, te, cfg["signal_var"], cfg["sigma_u"], cfg["sigma_w"], w0,
-                         cfg["m"], cfg["epsw"], cfg["epsU"], cfg["a"], cfg["b"], cfg["c"], 0,
-                         epochs, cfg["param_seed"], mu, sd)
-    dt = time.perf_counter() - t0
-    steps = epochs * -(-tr.shape[0] // cfg["m"])
-    return dict(value=steps / dt, unit="fold-steps/s (1 fold, 1 core)", cores=1, kind="port",
-                sample="oracle/movielens_ref.py (numpy restatement of "
-                       "100k_movielensExperiment.jl:409-551) on fold 1, %d epoch(s) = %d minibatch "
-                       "steps plus the per-epoch train / test evaluation, in %.1f s"
-                       % (epochs, steps, dt))
+    from oracle import philox as px
+    r = np.asarray(w0).shape[0]
+    ud, md = folds[0][2], folds[0][3]
+    n1, D1 = ud.shape
+    n2, D2 = md.shape
+    U0 = M.init_uv(n1 + D1, r, cfg["param_seed"], 0, False, cfg["sigma_u"])
+    V0 = M.init_uv(n2 + D2, r, cfg["param_seed"], 1, False, cfg["sigma_u"])
+    N = folds[0][0].shape[0]
+    perms = np.stack([px.randperm(N, cfg["param_seed"], e) for e in range(epochs)])
+    args = (ud, md)
+    hyper = (w0, U0, V0, cfg["signal_var"], cfg["sigma_u"], cfg["sigma_w"], cfg["m"], cfg["epsw"],
+             cfg["epsU"], cfg["a"], cfg["b"], cfg["c"])
+    nb = -(-N // cfg["m"])
+    sec1, _ = cpu_lib.cf_sgd_folds([(folds[0][0], folds[0][1])], *args, [perms[:2]], *hyper, threads=1)
+    nf = len(folds)
+    sec, _ = cpu_lib.cf_sgd_folds([(f[0], f[1]) for f in folds], *args, [perms] * nf, *hyper,
+                                  threads=nf)
+    return dict(value=nf * epochs * nb / sec, unit="fold-steps/s (%d folds on %d cores)" % (nf, nf),
+                cores=nf, kind="port", single_core_steps_per_s=2 * nb / sec1,
+                sample="oracle/cpu/movielens_cpu.cpp (C++ fp64 restatement of "
+                       "100k_movielensExperiment.jl:409-551, SGD, the reference's dense row "
+                       "moves) on the %d folds, %d epochs = %d minibatch steps per fold plus each "
+                       "epoch's train / test evaluation, one OpenMP thread per fold, in %.1f s; "
+                       "fold 1 alone on 1 core for 2 epochs in %.2f s"
+                       % (nf, epochs, epochs * nb, sec, sec1))
 
 
 def movielens_main(args):
@@ -481,7 +498,7 @@ def movielens_main(args):
         gr["frac"] = gr["achieved"] / gr["peak"]
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = movielens_cpu_baseline(folds[0], w0, cfg)
+        cpu = movielens_cpu_baseline(folds, w0, cfg)
     if rank == 0:
         nb = -(-trs[0].shape[0] // cfg["m"])
         out = {

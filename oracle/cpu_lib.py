@@ -25,6 +25,11 @@ def lib():
         L.gptcpu_regression.argtypes = [C.POINTER(C.c_int64), P_D, P_D, P_D, C.POINTER(C.c_int32),
                                         C.c_int, C.POINTER(C.c_uint64), C.c_int, P_D, P_D, P_D, P_D,
                                         C.POINTER(C.c_int32), P_D]
+        L.gptcpu_cf_sgd.restype = C.c_double
+        PP_I = C.POINTER(C.POINTER(C.c_int32))
+        PP_D = C.POINTER(C.POINTER(C.c_double))
+        L.gptcpu_cf_sgd.argtypes = [C.c_int, C.POINTER(C.c_int64), P_D] + [C.POINTER(C.c_int32)] * 4 + \
+            [PP_I, PP_I, PP_D, PP_I, PP_I, PP_I, PP_D, PP_D, PP_D, PP_D, PP_D, C.c_int]
         L.gptcpu_max_threads.restype = C.c_int
         L.gptcpu_pred.restype = None
         L.gptcpu_pred.argtypes = [C.c_int64] * 6 + [P_D, P_D, P_D, C.POINTER(C.c_int32), C.c_int,
@@ -94,3 +99,63 @@ def cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def _csr(data, base):
+    """CSR of the feature rows of each user / movie (absolute U / V rows base + f)."""
+    ptr, fe = [0], []
+    for row in np.asarray(data):
+        fe.extend(int(base + f) for f in np.flatnonzero(row))
+        ptr.append(len(fe))
+    return np.array(ptr, dtype=np.int32), np.array(fe if fe else [0], dtype=np.int32)
+
+
+def cf_sgd_folds(folds, UserData, MovieData, perms, w0, U0, V0, signal_var, sigma_u, sigma_w, m,
+                 epsw, epsU, a, b, c, threads=1):
+    """GPT_fullw_sideinfo SGD epochs (langevin = stiefel = false) of every fold on ``threads``
+    OpenMP threads, from the given state: folds = [(Rating, Ratingtest)] (1-based ids,
+    standardised ratings), perms[f] = (epochs, N) 0-based orders, w0 (r, r), U0 / V0 (rows, r)
+    row-major starting states shared by the folds.  Returns (seconds, [(w, U, V, sse (epochs, 2))])."""
+    L = lib()
+    nf = len(folds)
+    n1, D1 = np.asarray(UserData).shape
+    n2, D2 = np.asarray(MovieData).shape
+    r = np.asarray(w0).shape[0]
+    uptr, ufe = _csr(UserData, n1)
+    vptr, vfe = _csr(MovieData, n2)
+    keep, outs = [], []
+    arr = {k: [] for k in ("u", "m", "y", "p", "tu", "tm", "ty", "w", "U", "V", "s")}
+    N = len(folds[0][0])
+    Nt = min(len(f[1]) for f in folds)
+    epochs = np.asarray(perms[0]).shape[0]
+    for f, (Rt, Rs) in enumerate(folds):
+        Rt = np.asarray(Rt, dtype=np.float64)
+        Rs = np.asarray(Rs, dtype=np.float64)[:Nt]
+        d = dict(u=np.ascontiguousarray(Rt[:, 0] - 1, dtype=np.int32),
+                 m=np.ascontiguousarray(Rt[:, 1] - 1, dtype=np.int32),
+                 y=np.ascontiguousarray(Rt[:, 2]),
+                 p=np.ascontiguousarray(perms[f], dtype=np.int32),
+                 tu=np.ascontiguousarray(Rs[:, 0] - 1, dtype=np.int32),
+                 tm=np.ascontiguousarray(Rs[:, 1] - 1, dtype=np.int32),
+                 ty=np.ascontiguousarray(Rs[:, 2]),
+                 w=np.array(w0, dtype=np.float64, order="F"),
+                 U=np.array(U0, dtype=np.float64, order="C"),
+                 V=np.array(V0, dtype=np.float64, order="C"),
+                 s=np.zeros((epochs, 2)))
+        keep.append(d)
+        for k in arr:
+            t = C.c_int32 if d[k].dtype == np.int32 else C.c_double
+            arr[k].append(_p(d[k], t))
+    def pp(k, t):
+        return (C.POINTER(t) * nf)(*arr[k])
+    icfg = np.array([N, Nt, n1, D1, n2, D2, r, m, epochs], dtype=np.int64)
+    dcfg = np.array([signal_var, sigma_u, sigma_w, epsw, epsU, a, b, c], dtype=np.float64)
+    sec = L.gptcpu_cf_sgd(nf, _p(icfg, C.c_int64), _p(dcfg), _p(uptr, C.c_int32), _p(ufe, C.c_int32),
+                          _p(vptr, C.c_int32), _p(vfe, C.c_int32), pp("u", C.c_int32),
+                          pp("m", C.c_int32), pp("y", C.c_double), pp("p", C.c_int32),
+                          pp("tu", C.c_int32), pp("tm", C.c_int32), pp("ty", C.c_double),
+                          pp("w", C.c_double), pp("U", C.c_double), pp("V", C.c_double),
+                          pp("s", C.c_double), int(threads))
+    for d in keep:
+        outs.append((d["w"], d["U"], d["V"], d["s"]))
+    return sec, outs

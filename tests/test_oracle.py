@@ -360,3 +360,33 @@ def test_kronecker_precision_from_user_statistics():
     rhs = np.einsum("ua,ub->ab", h, U).reshape(r * r)
     assert np.abs(Z - K.T @ K).max() <= 1e-12 * np.abs(K.T @ K).max()
     assert np.abs(rhs - K.T @ y).max() <= 1e-12 * np.abs(K.T @ y).max()
+
+
+def test_movielens_cpp_port_matches_numpy_restatement():
+    """oracle/cpu/movielens_cpu.cpp (the MovieLens CPU baseline of bench.py) against
+    oracle/movielens_ref.py's GPT_fullw_sideinfo (SGD) over two epochs of a small problem."""
+    from oracle import cpu_lib
+    from oracle import movielens_ref as M
+    from oracle import philox as px
+    rng = np.random.default_rng(3)
+    n1, n2, D1, D2, r, N, Nt, m, seed = 30, 40, 5, 4, 4, 300, 50, 16, 17
+    ud = (rng.random((n1, D1)) < 0.3).astype(float)
+    md = (rng.random((n2, D2)) < 0.3).astype(float)
+
+    def ratings(n):
+        return np.column_stack([rng.integers(1, n1 + 1, n), rng.integers(1, n2 + 1, n),
+                                rng.standard_normal(n)])
+    R, Rt = ratings(N), ratings(Nt)
+    w0 = 0.3 * rng.standard_normal((r, r))
+    want = M.GPT_fullw_sideinfo(R, ud, md, Rt, 0.8, 0.1, 1.0, w0, m, 1e-3, 1e-3, 0.5, 0.25, 0.5, 0,
+                                2, seed, 0.0, 1.0)
+    U0 = M.init_uv(n1 + D1, r, seed, 0, False, 0.1)
+    V0 = M.init_uv(n2 + D2, r, seed, 1, False, 0.1)
+    perms = np.stack([px.randperm(N, seed, e) for e in range(2)])
+    _, outs = cpu_lib.cf_sgd_folds([(R, Rt)], ud, md, [perms], w0, U0, V0, 0.8, 0.1, 1.0, m, 1e-3,
+                                   1e-3, 0.5, 0.25, 0.5)
+    w, U, V, sse = outs[0]
+    for got, ref in ((w, want[0][:, :, 1]), (U, want[1][:, :, 1]), (V, want[2][:, :, 1])):
+        assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
+    pred = M.predict(Rt, U, V, w, *M.side_rows(ud, md), 0.5, 0.25, 0.5)
+    assert sse[1, 1] == pytest.approx(np.sum((Rt[:, 2] - pred) ** 2), rel=1e-12)
