@@ -319,6 +319,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
   double* Fl = nullptr;
   double* Fc = nullptr;
   unsigned long long* hit = nullptr;
+  double* mcl = nullptr;   // the batch's own U / V rows as of this step, [side][ii][l] (sums phase)
   if (lazy) {
     const size_t o0 = cf_lazy_offset(R, m, nfeat);
     cpow = (double*)(smem + o0);
@@ -326,6 +327,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     Fl = (double*)(smem + ((o0 + 8 * ((size_t)nb + 1) + 4 * (size_t)(P.rowsU + P.rowsV) + 15) / 16 * 16));
     Fc = Fl + nfeat * R;
     hit = (unsigned long long*)(Fc + nfeat * R);
+    mcl = (double*)(hit + 2);                          // 2 · m · R
     const double lc = log1p(-P.epsU / (2 * su2));
     for (int d = tid; d <= nb; d += kCfNT) cpow[d] = d == 0 ? 1.0 : exp((double)d * lc);
     for (int o = tid; o < P.rowsU + P.rowsV; o += kCfNT) cur[o] = 0;
@@ -334,28 +336,100 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       Fl[o] = gptr(side ? C.V : C.U)[(side ? P.n2 : P.n1) + f + (size_t)(side ? P.rowsV : P.rowsU) * l];
     }
   }
+  // lazy path: the next batch's (user, movie, rating) of thread tid < m are loaded during this
+  // step's gradient phase and their feature masks after it, so the batch and mask phases of the
+  // next step wait for no global memory (the barriers between them wait for LDS only)
+  int pf_u = 0, pf_m = 0;
+  double pf_r = 0.0;
+  uint64_t pf_mu = 0, pf_mm = 0;
+  auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
   for (int bt = bt0; bt < bt0 + nb; ++bt) {
     CF_STAMP(bt, 0);
     const long long step = step0 + (bt - bt0);
     const int jl = bt - bt0;                           // launch-local step (lazy move)
     const int B = min(m, N - bt * m);
     const double cN = (double)N / (double)B;
-    for (int ii = tid; ii < B; ii += kCfNT) {
-      us[ii] = C.ep_user[bt * m + ii];                // the epoch's order (cf_gather_kernel)
-      ms[ii] = C.ep_movie[bt * m + ii];
-      er[ii] = C.ep_rating[bt * m + ii];
+    const bool pref = lazy && bt > bt0 && m <= kCfNT;  // this batch was prefetched
+    if (pref) {
+      if (tid < B) {
+        us[tid] = pf_u;
+        ms[tid] = pf_m;
+        er[tid] = pf_r;
+        umk[tid] = pf_mu;
+        vmk[tid] = pf_mm;
+      }
+    } else {
+      for (int ii = tid; ii < B; ii += kCfNT) {
+        us[ii] = C.ep_user[bt * m + ii];              // the epoch's order (cf_gather_kernel)
+        ms[ii] = C.ep_movie[bt * m + ii];
+        er[ii] = C.ep_rating[bt * m + ii];
+      }
     }
     if (lazy && tid < 2) hit[tid] = 0ull;
-    __syncthreads();
+    if (pref) lds_barrier(); else __syncthreads();
     CF_STAMP(bt, 1);
     // per (side, ii): the feature bitmask, the first-occurrence flag and the next occurrence
+    if (B <= 128) {
+      // the links by sorting: wave `side` sorts the 128 keys (id << 8 | position) of its side
+      // (two per lane, bitonic, lane exchanges by __shfl_xor), so equal ids end up adjacent in
+      // ascending position: a key's successor with the same id is its next occurrence, and a key
+      // whose predecessor differs is the first (the round-4 form compared every pair, 11.6 k
+      // cycles of the step); the masks go to LDS from the other waves
+      const int wv = uni(tid >> 6), lane = tid & 63;
+      if (wv < 2) {
+        const int* ids = wv ? ms : us;
+        int k0 = lane < B ? (ids[lane] << 8) | lane : 0x7fffffff;
+        int k1 = lane + 64 < B ? (ids[lane + 64] << 8) | (lane + 64) : 0x7fffffff;
+#pragma unroll
+        for (int k = 2; k <= 128; k <<= 1) {
+#pragma unroll
+          for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j == 64) {                             // (k = 128: ascending everywhere)
+              const int lo = min(k0, k1), hi = max(k0, k1);
+              k0 = lo;
+              k1 = hi;
+            } else {
+              const int o0 = __shfl_xor(k0, j), o1 = __shfl_xor(k1, j);
+              const bool low = (lane & j) == 0;        // this element is the lower of its pair
+              const bool asc0 = (lane & k) == 0, asc1 = ((lane + 64) & k) == 0;
+              k0 = (low == asc0) ? min(k0, o0) : max(k0, o0);
+              k1 = (low == asc1) ? min(k1, o1) : max(k1, o1);
+            }
+          }
+        }
+        // neighbours in sorted order: e = lane (k0) and e = 64 + lane (k1)
+        const int p0 = __shfl(k0, (lane + 63) & 63), p1 = __shfl(k1, (lane + 63) & 63);
+        const int n0 = __shfl(k0, (lane + 1) & 63), n1 = __shfl(k1, (lane + 1) & 63);
+        const int last0 = __shfl(k0, 63), first1 = __shfl(k1, 0);   // with every lane active
+        const int prev0 = lane == 0 ? 0x7fffffff : p0, prev1 = lane == 0 ? last0 : p1;
+        const int next0 = lane == 63 ? first1 : n0, next1 = lane == 63 ? 0x7fffffff : n1;
+        int* nxl = wv ? vnx : unx;
+        auto link = [&](int key, int prev, int next) {
+          if (key == 0x7fffffff) return;
+          const bool first = (prev >> 8) != (key >> 8) || prev == 0x7fffffff;
+          const int nx = (next != 0x7fffffff && (next >> 8) == (key >> 8)) ? (next & 0xff) : -1;
+          nxl[key & 0xff] = (nx + 1) | (first ? 1 << 16 : 0);
+        };
+        link(k0, prev0, next0);
+        link(k1, prev1, next1);
+      } else if (masks) {
+        for (int o = tid - 128; o < 2 * B; o += kCfNT - 128) {
+          const int side = o >= B ? 1 : 0, ii = o - side * B;
+          const int id = (side ? ms : us)[ii];
+          const uint64_t mk = pref ? (side ? vmk : umk)[ii] : (side ? P.vmask : P.umask)[id];
+          if (!pref) (side ? vmk : umk)[ii] = mk;
+          if (lazy) __hip_atomic_fetch_or(hit + side, (unsigned long long)mk, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    } else
     for (int o = tid; o < 2 * B; o += kCfNT) {
       const int side = o >= B ? 1 : 0, ii = o - side * B;
       const int* ids = side ? ms : us;
       const int id = ids[ii];
       if (masks) {
-        const uint64_t mk = (side ? P.vmask : P.umask)[id];
-        (side ? vmk : umk)[ii] = mk;
+        const uint64_t mk = pref ? (side ? vmk : umk)[ii] : (side ? P.vmask : P.umask)[id];
+        if (!pref) (side ? vmk : umk)[ii] = mk;
         if (lazy) __hip_atomic_fetch_or(hit + side, (unsigned long long)mk, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -406,6 +480,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
           const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
           const int id = side ? ms[ii] : us[ii];
           const double mcur = mv[k4] * cpow[jl - cur[(side ? P.rowsU : 0) + id]];
+          mcl[o] = mcur;                                 // o = (side·B + ii)·R + l
           const double* Fs = Fc + (side ? P.D1 * R : 0) + l;
           uint64_t mk = (side ? vmk : umk)[ii];
           double f = 0.0;
@@ -544,6 +619,12 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     }
     __syncthreads();
     CF_STAMP(bt, 5);
+    const int Bn = bt + 1 < bt0 + nb ? min(m, N - (bt + 1) * m) : 0;
+    if (lazy && m <= kCfNT && tid < Bn) {             // the next batch, in flight under the gradients
+      pf_u = C.ep_user[(bt + 1) * m + tid];
+      pf_m = C.ep_movie[(bt + 1) * m + tid];
+      pf_r = C.ep_rating[(bt + 1) * m + tid];
+    }
     // gradw (:466, :473-477) and the w step of :479-483 into wn
     // (GPT_fixw / GPT_fixw_sideinfo, :56-156 / :282-404: w is fixed — no gradw, no step)
     // gradw[i, j] = Σ_ii sumU[ii, i]·(er_ii·sumV[ii, j]) on the fp64 matrix cores: one wave per
@@ -599,7 +680,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       const size_t e = id + (size_t)(side ? P.rowsV : P.rowsU) * l;
       if (lazy) {                                     // the row's move of this step (cf_move)
         double* M = side ? C.V : C.U;
-        const double m0 = gptr(M)[e] * cpow[jl - cur[(side ? P.rowsU : 0) + id]];
+        const double m0 = mcl[o];                     // the value the sums phase read (no update since)
         gptr_w(M)[e] = m0 + P.epsU * (g * cN - m0 / su2) / 2;
       } else {
         gptr_w(side ? C.GV : C.GU)[e] = g * cN;
@@ -685,6 +766,10 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     }
     __syncthreads();
     CF_STAMP(bt, 6);
+    if (lazy && m <= kCfNT && tid < Bn) {             // ... and its feature masks
+      pf_mu = P.umask[pf_u];
+      pf_mm = P.vmask[pf_m];
+    }
     if (lazy) {                                       // the moved rows are current as of jl + 1
       for (int o = tid; o < 2 * B; o += kCfNT) {
         const int side = o >= B ? 1 : 0, ii = o - side * B;
@@ -702,7 +787,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     }
     CF_STAMP(bt, 7);
     for (int o = tid; o < R * R; o += kCfNT) w_l[o] = wn_l[o];
-    __syncthreads();
+    if (lazy) lds_barrier(); else __syncthreads();    // (no global writes since the last fence)
   }
   if (lazy) {                                         // every row brought to the launch's end
     const int nUe = P.rowsU * R;
@@ -1142,7 +1227,7 @@ size_t cf_lds_bytes(int r, int m, int nfeat, bool masks) {
 // the feature rows Fl, Fc (nfeat × r each) and the two hit masks
 size_t cf_lazy_lds_bytes(int r, int m, int nfeat, int rows, int nb) {
   return al16(cf_lazy_offset(r, m, nfeat) + 8 * ((size_t)nb + 1) + 4 * (size_t)rows) +
-         16 * (size_t)nfeat * r + 16 + 16;
+         16 * (size_t)nfeat * r + 16 + 16 + 16 * (size_t)m * r;
 }
 
 bool cf_rank_supported(int r) {
