@@ -693,7 +693,8 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       constexpr int LT = (R + 15) / 16;
       const int lane = tid & 63, wv = uni(tid >> 6), rl = lane & 15, kl = lane >> 4;
       const int FT1 = (P.D1 + 15) / 16, FT2 = (P.D2 + 15) / 16;
-      for (int t = wv; t < (FT1 + FT2) * LT; t += kCfNW) {
+      // tiles from the last wave down, so they do not queue behind gradw's tiles on waves 0, 1, ..
+      for (int t = kCfNW - 1 - wv; t < (FT1 + FT2) * LT; t += kCfNW) {
         const int ft = t / LT, lt = t - ft * LT, side = ft >= FT1 ? 1 : 0;
         const int f0 = (ft - side * FT1) * 16, Ds = side ? P.D2 : P.D1;
         int zo = 0;
