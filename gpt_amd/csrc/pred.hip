@@ -728,7 +728,11 @@ static hipError_t launch_vphase_rows(const double* w, const double* T, const int
     const char* ev = std::getenv("GPTSGLD_PRED_ROWS_PF");
     return !(ev && std::strcmp(ev, "0") == 0);
   }();
-  if (pf && D * r <= kRowsPfWaves * 16) {
+  // (the persistent kernel's LDS: the tile's rows, the wave partials, the entries' offsets and
+  // the sample's w — a large core (Q·D) can push it past one CU's 160 KB)
+  const size_t pf_lds = 8 * (size_t)D * r * 64 + 8 * (size_t)kRowsPfWaves * 64 +
+                        4 * (((size_t)Q * D + 3) & ~(size_t)3) + 8 * (size_t)Q;
+  if (pf && D * r <= kRowsPfWaves * 16 && pf_lds <= 160 * 1024) {
     // rows per wave: 10 (D·r ≤ 160: kin40kExperiment.jl's D = 8, r = 20) or 16
     if (D * r <= kRowsPfWaves * 10) {
       switch (D) {

@@ -79,6 +79,10 @@ for s in "$@"; do
     rowsabl) for a in 0 1 2 0; do run rowsabl_$a 200 env GPTSGLD_ROWS_ABL=$a $RP -d gpurun_out/${T}_prof_rabl$a -o r -- python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 3; done ;;
     allocab) for a in pool plain pool plain; do run allocab_$a 200 env GPTSGLD_PRED_ALLOC=$a $RP -d gpurun_out/${T}_prof_alloc_$a -o r -- python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 3; done ;;
     nwab) for a in 8 16 8 16; do run nwab_$a 200 env GPTSGLD_PRED_ROWS_NW=$a $RP -d gpurun_out/${T}_prof_nw$a -o r -- python -u scripts/time_pred.py --S 224 --n 150 --r 20 --tiles 44 --vphases rows --reps 3; done ;;
+    wvhead) for v in head new head new; do
+              if [ $v = head ]; then L=gpt_amd/libgptsgld_head.so; else L=gpt_amd/libgptsgld.so; fi
+              run wvhead_$v 200 env GPTSGLD_LIB=$L python -u scripts/wave_probe.py --chains 256 --engines wave --steps 400
+            done ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s" ;;
   esac
