@@ -83,6 +83,7 @@ for s in "$@"; do
               if [ $v = head ]; then L=gpt_amd/libgptsgld_head.so; else L=gpt_amd/libgptsgld.so; fi
               run wvhead_$v 200 env GPTSGLD_LIB=$L python -u scripts/wave_probe.py --chains 256 --engines wave --steps 400
             done ;;
+    bailtest) run bailtest 300 $PYT tests/test_gpu_quality.py -k "bailouts_match" ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s" ;;
   esac
