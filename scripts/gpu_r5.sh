@@ -84,6 +84,7 @@ for s in "$@"; do
               run wvhead_$v 200 env GPTSGLD_LIB=$L python -u scripts/wave_probe.py --chains 256 --engines wave --steps 400
             done ;;
     bailtest) run bailtest 300 $PYT tests/test_gpu_quality.py -k "bailouts_match" ;;
+    chainsab) for c in 256 288 320; do run chainsab_$c 300 python -u bench.py --workload kin40k_ref --chains $c --no-cpu-baseline --no-single-chain; done ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s" ;;
   esac
