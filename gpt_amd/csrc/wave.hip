@@ -971,12 +971,21 @@ __global__ __launch_bounds__(64, 1) void wv_dim_kernel(StepParams P,
   for (int x = 0; x < MXL; ++x)
     if (lane + 64 * x < R * R) mx[lane + 64 * x] = mxr[x];
   wave_sync();
-  for (int o = lane; o < NN * R; o += 64) {
-    const int a = o / R, l = o - a * R;
-    double s = 0.0;
-#pragma unroll 4
-    for (int c2 = 0; c2 < R; ++c2) s = fma(S1[a * NN + c2], mx[c2 * R + l], s);
-    F[o] = s;
+  // one row of F per lane (a = lane < 2r): R independent fma chains, each over c2 in order (the
+  // same doubles as one output per lane and pass); the expm(−tA) rows are wave-uniform reads
+  if (lane < NN) {
+    const int a = lane;
+    double acc[R];
+#pragma unroll
+    for (int l = 0; l < R; ++l) acc[l] = 0.0;
+#pragma unroll 2
+    for (int c2 = 0; c2 < R; ++c2) {
+      const double e = S1[a * NN + c2];
+#pragma unroll
+      for (int l = 0; l < R; ++l) acc[l] = fma(e, mx[c2 * R + l], acc[l]);
+    }
+#pragma unroll
+    for (int l = 0; l < R; ++l) F[a * R + l] = acc[l];
   }
   wave_sync();
   if (bad) {                                             // NaN in the geodesic (:422-424)
