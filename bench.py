@@ -307,9 +307,7 @@ def compose_line(v):
         "pred": {"samples": v.npred, "Ntest": v.Nte, "ms": v.pred_ms, "gemm_flop": v.pred_flop,
                  "achieved_tflops": pred_tfs, "peak_tflops": FP64_MFMA_PEAK_TFS,
                  "frac": pred_tfs / FP64_MFMA_PEAK_TFS,
-                 "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + %s" % (
-                     "pred_vphase_pairs_kernel" if v.r <= 5 and -(-v.D // 2) <= 8
-                     else "pred_vphase_rows_kernel"),
+                 "kernels": "pred_temp_mfma_kernel (v_mfma_f64_16x16x4f64) + %s" % v.vphase_kernel,
                  "note": "whole stacked-sample call timed with events (GEMM + V-phase), median of 5 calls after 3 warm-up calls (the GEMM's clock settles over the first calls: 6.1, 5.6, 5.3 ms in profiles/r5ak_kernel_stats.csv's trace)",
                  "gemm_ms": v.gemm_ms, "vphase_ms": v.vphase_ms,
                  "gemm_roofline": {"bound": "mfma", "achieved": gemm_tfs,
@@ -853,7 +851,8 @@ def main():
         pred_times.append(ev0.elapsed_time(ev1))
     pred_ms = sorted(pred_times)[2]
     pred_flop = 2.0 * npred * r * n * D * Nte             # the GEMM (dominant); V-phase excluded
-    from gpt_amd.session import pred_device_timed
+    from gpt_amd.session import pred_device_timed, pred_last_vphase
+    vphase_kernel = pred_last_vphase()               # the kernel the calls above launched
     gemm_ms, vphase_ms = pred_device_timed(w_all.data_ptr(), U_all.data_ptr(), I0, phi_te, n, D,
                                            Nte, r, Q, npred, fh)
     fsum = fh.sum(dim=0)
@@ -903,6 +902,7 @@ def main():
             k_us_ranks=k_us_ranks, bytes_launch=bytes_launch, steps_run=steps_run, cpu=cpu,
             quality=quality, allreduce_ms=allreduce_ms, npred=npred, pred_ms=pred_ms,
             pred_flop=pred_flop, gemm_ms=gemm_ms, vphase_ms=vphase_ms, rmse_final=rmse_final,
+            vphase_kernel=vphase_kernel,
             single=single))
         print(json.dumps(out))
     sess.close()

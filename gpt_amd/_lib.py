@@ -70,6 +70,7 @@ SIGNATURES = {
     "gpt_pred_trim_pool": (C.c_int, []),
     "gpt_cf_last_timing": (C.c_int, [P_D, P_D, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "gpt_cf_last_mode": (C.c_int, [C.POINTER(C.c_int32)]),
+    "gpt_pred_last_vphase": (C.c_int, [C.POINTER(C.c_int32)]),
     "gpt_cf_last_stamps": (C.c_int64, [C.POINTER(C.c_int64), C.c_int64]),
     "gpt_sgld_session_timeline": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(C.c_int64), P_D]),
     "gpt_feature_dev": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,

@@ -1806,6 +1806,8 @@ static int cf_sgd_run(
   std::vector<char> live(F, 1);
   std::vector<int> testcounter(F, 0);
   int counter = 0, nlive = F;
+  long long step_base_host = 0;                      // graph replays' epoch base: read by the copy
+                                                     // below, alive until the epoch's event sync
   const int32_t stopped = 2;                         // skips the fold in later launches
   struct Events {
     hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -1834,7 +1836,10 @@ static int cf_sgd_run(
   // SGD (no Langevin noise, no Stiefel geometry) on the feature-mask path: the lazy move, one
   // launch per epoch (cf_epoch_kernel domove = 2); GPTSGLD_CF_LAZY=0 keeps the batch-phase / move
   // launch pairs
-  const bool lazy = !stiefel && !langevin && P.umask != nullptr &&
+  // (the decay factor c = 1 − εU/(2σ_u²) of a skipped row must lie in (0, 1): the kernel reads a
+  // row Δ steps behind as m·c^Δ; outside that range the eager move keeps the reference's numbers)
+  const double cdecay = 1.0 - P.epsU / (2.0 * P.sigma_u * P.sigma_u);
+  const bool lazy = !stiefel && !langevin && P.umask != nullptr && cdecay > 0.0 && cdecay < 1.0 &&
                     cf_lazy_lds_bytes((int)r, (int)m, (int)(D1 + D2), rowsU + rowsV, nbatch) <=
                         160 * 1024 &&
                     !(std::getenv("GPTSGLD_CF_LAZY") && std::strcmp(std::getenv("GPTSGLD_CF_LAZY"), "0") == 0);
@@ -1876,8 +1881,8 @@ static int cf_sgd_run(
         if (ec != hipSuccess) return hip_fail(ec, "hipStreamEndCapture");
         HIPCHK(hipGraphInstantiate(&rs.x, rs.g, nullptr, nullptr, 0));
       }
-      const long long base = (epoch - 1) * nbatch;
-      HIPCHK(hipMemcpyAsync(d_step.p, &base, sizeof(long long), hipMemcpyHostToDevice, st));
+      step_base_host = (epoch - 1) * nbatch;
+      HIPCHK(hipMemcpyAsync(d_step.p, &step_base_host, sizeof(long long), hipMemcpyHostToDevice, st));
       HIPCHK(hipEventRecord(evs.e[0], st));
       e = hipGraphLaunch(rs.x, st);
     }
@@ -2026,6 +2031,12 @@ extern "C" int gpt_cf_last_timing(double* epoch_ms, double* eval_ms, int64_t* ep
   *eval_ms = g_cf_timing.eval_ms;
   *epochs = g_cf_timing.epochs;
   *fold_steps = g_cf_timing.fold_steps;
+  return GPT_OK;
+}
+
+extern "C" int gpt_pred_last_vphase(int32_t* kind) {
+  if (!kind) { set_error("gpt_pred_last_vphase: null output"); return GPT_ERR_BAD_DIMS; }
+  *kind = pred_last_vphase();
   return GPT_OK;
 }
 
@@ -2243,11 +2254,36 @@ static int cf_gibbs_run(
   double* krm = ktp + (size_t)Ntest * chunkE;
   std::vector<double> rm(2 * (size_t)chunkE);
   int64_t flushed = 0;                              // kept sweeps already in the caller's arrays
+  // Julia throws PosDefException (no outputs): every output array is zeroed before the error
+  auto not_spd = [&]() -> int {
+    if (w_store) std::memset(w_store, 0, 8 * rr * maxepoch);
+    std::memset(U_store, 0, 8 * nU * maxepoch);
+    std::memset(V_store, 0, 8 * nV * maxepoch);
+    std::memset(testpred_store, 0, 8 * (size_t)Ntest * maxepoch);
+    std::memset(trainRMSE, 0, 8 * (size_t)maxepoch);
+    std::memset(testRMSE, 0, 8 * (size_t)maxepoch);
+    set_error("PosDefException: a Gibbs precision matrix is not positive definite");
+    return GPT_ERR_NOT_SPD;
+  };
+  // The status word after every epoch's sweeps is copied into pinned memory behind them and read
+  // one epoch later, so a failed Cholesky stops the sampler within two epochs without a full
+  // synchronisation per epoch.
+  struct StatusRing {
+    int32_t* h = nullptr;
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~StatusRing() {
+      for (auto x : e) if (x) (void)hipEventDestroy(x);
+      if (h) (void)hipHostFree(h);
+    }
+  } sr;
+  HIPCHK(hipHostMalloc((void**)&sr.h, 2 * sizeof(int32_t), hipHostMallocDefault));
+  sr.h[0] = sr.h[1] = 0;
+  for (auto& x : sr.e) HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
   auto flush = [&](int64_t upto) -> int {
     HIPCHK(hipStreamSynchronize(nullptr));
     int32_t bad = 0;
     HIPCHK(hipMemcpy(&bad, d_st.p, 4, hipMemcpyDeviceToHost));
-    if (bad) { set_error("PosDefException: a Gibbs precision matrix is not positive definite"); return GPT_ERR_NOT_SPD; }
+    if (bad) return not_spd();
     const int64_t c = upto - flushed;
     if (c <= 0) return GPT_OK;
     if (w_store) HIPCHK(hipMemcpy(w_store + rr * flushed, kw, 8 * rr * c, hipMemcpyDeviceToHost));
@@ -2305,9 +2341,16 @@ static int cf_gibbs_run(
         const int rc = flush(s2 + 1);
         if (rc != GPT_OK) return rc;
       }
-    } else if (epoch % 64 == 0) {           // a long burn-in still reports a non-SPD draw early
-      const int rc = flush(flushed);
-      if (rc != GPT_OK) return rc;
+    }
+    const int ring = (int)(epoch & 1);
+    HIPCHK(hipMemcpyAsync(sr.h + ring, d_st.p, 4, hipMemcpyDeviceToHost, nullptr));
+    HIPCHK(hipEventRecord(sr.e[ring], nullptr));
+    if (epoch > 1) {                        // the previous epoch's status, one epoch behind
+      HIPCHK(hipEventSynchronize(sr.e[ring ^ 1]));
+      if (sr.h[ring ^ 1]) {
+        HIPCHK(hipStreamSynchronize(nullptr));
+        return not_spd();
+      }
     }
   }
   return flush(maxepoch);

@@ -328,8 +328,16 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     Fc = Fl + nfeat * R;
     hit = (unsigned long long*)(Fc + nfeat * R);
     mcl = (double*)(hit + 2);                          // 2 · m · R
-    const double lc = log1p(-P.epsU / (2 * su2));
-    for (int d = tid; d <= nb; d += kCfNT) cpow[d] = d == 0 ? 1.0 : exp((double)d * lc);
+    // c^d by binary powering (the host takes this path only for 0 < c < 1)
+    const double c1 = 1.0 - P.epsU / (2 * su2);
+    for (int d = tid; d <= nb; d += kCfNT) {
+      double p = 1.0, b = c1;
+      for (int e = d; e > 0; e >>= 1) {
+        if (e & 1) p *= b;
+        b *= b;
+      }
+      cpow[d] = p;
+    }
     for (int o = tid; o < P.rowsU + P.rowsV; o += kCfNT) cur[o] = 0;
     for (int o = tid; o < nfeat * R; o += kCfNT) {
       const int fo = o / R, l = o - fo * R, side = fo >= P.D1 ? 1 : 0, f = fo - side * P.D1;

@@ -928,6 +928,9 @@ __device__ bool wave_expm(double* S, long long* st = nullptr) {
 #pragma unroll
     for (int i = 0; i < NN; ++i) cs += fabs(A[i * NN + lane]);
   }
+  // a non-finite ‖A‖₁ (an Inf or NaN entry): the oracle's NaN result (Julia's expm! would throw at
+  // ceil(Int, log2(nA/5.4))), i.e. geod's bail-out; wave_max (fmax) alone would drop a NaN column
+  if (__any(!(cs <= 1.79769313486231570e308))) return true;
   const double nA = wave_max(cs);
   int si = 0;
   if (nA <= 2.1) {
@@ -959,9 +962,9 @@ __device__ bool wave_expm(double* S, long long* st = nullptr) {
     for (int o = lane; o < q; o += 64) U[o] = A6[o];
     wave_sync();
   } else {
+    // as many squarings as Julia's expm! takes (no cap; ‖A‖₁ <= DBL_MAX bounds si by 1022)
     const double s = log2(nA / 5.4);
-    si = (s > 0.0) ? (s < 60.0 ? (int)ceil(s) : 60) : 0;
-    if (!(nA == nA)) si = 0;
+    si = (s > 0.0) ? (int)ceil(s) : 0;
     if (st && lane == 0) st[10] = 13 + 100 * si;
     if (si > 0) {
       const double sc = ldexp(1.0, -si);

@@ -215,6 +215,7 @@ size_t pred_x_lds_bytes(int n, int D, int r, int Q);
 // Per-phase event timing of the stacked-sample prediction (diagnostics / the benchmark):
 // gemm_ms / vphase_ms accumulate over the sample chunks of one call.
 struct PredPhaseTiming { double gemm_ms = 0.0, vphase_ms = 0.0; };
+int pred_last_vphase();
 hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, const double* phitest,
                        int n, int D, long long Ntest, int r, int Q, int S, double* fhat,
                        hipStream_t st, PredPhaseTiming* timing = nullptr);

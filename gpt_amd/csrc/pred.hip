@@ -696,6 +696,12 @@ static hipError_t vphase_pairs(int NTp, const double* w, const double* T, const 
   }
 }
 
+// Which V-phase kernel the last prediction call on this thread launched (gpt_pred_last_vphase):
+// 0 pred_vphase_pairs_kernel, 1 pred_vphase_rows_pf_kernel, 2 pred_vphase_rows_kernel,
+// 3 pred_vphase_kernel (tile), 4 pred_kernel (direct, no separate V-phase).
+static thread_local int g_pred_vphase = -1;
+int pred_last_vphase() { return g_pred_vphase; }
+
 // The rows V-phase: the persistent prefetching kernel while a tile's D·R rows fit 16 per wave
 // (GPTSGLD_PRED_ROWS_PF=0: the one-tile-per-workgroup kernel, for comparison), as many workgroups
 // as the LDS lets every CU hold.
@@ -707,6 +713,7 @@ static hipError_t launch_rows_pf(const double* w, const double* T, const int32_t
   hipError_t e =
       set_max_lds_once((const void*)pred_vphase_rows_pf_kernel<DD, NW, NPW>, 160 * 1024, attr);
   if (e != hipSuccess) return e;
+  g_pred_vphase = 1;
   int dev = 0, cus = 0;
   e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -749,6 +756,7 @@ static hipError_t launch_vphase_rows(const double* w, const double* T, const int
     const hipError_t e = set_max_lds_once((const void*)pred_vphase_rows_kernel, 160 * 1024, attr);
     if (e != hipSuccess) return e;
   }
+  g_pred_vphase = 2;
   hipLaunchKernelGGL(pred_vphase_rows_kernel, dim3((unsigned)((Ntest + 63) / 64), Sc),
                      dim3(64 * kRowsWaves), rlds, st, w, T, offs, D, r, Ntest, Q, fhat);
   return hipGetLastError();
@@ -879,6 +887,7 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     if (timing) (void)hipEventRecord(ev[1], st);
     dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
     if (pairs) {
+      g_pred_vphase = 0;
       e = vphase_pairs(NTp, w + (size_t)s0 * Q, T, offp, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest,
                        Sc, Ntest, plds, st);
       if (timing && e == hipSuccess) {
@@ -906,6 +915,7 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
       }
       continue;
     }
+    g_pred_vphase = 3;
     switch (r) {
 #define CASE(RR)                                                                             \
   case RR: {                                                                                 \
@@ -963,7 +973,10 @@ hipError_t launch_pred(const double* w, const double* U, const int32_t* I0, cons
     const char* ev = std::getenv("GPTSGLD_PRED");
     return ev && std::strcmp(ev, "direct") == 0;
   }();
-  if (direct) return launch_pred_direct(w, U, I0, phitest, n, D, Ntest, r, Q, S, fhat, st);
+  if (direct) {
+    g_pred_vphase = 4;
+    return launch_pred_direct(w, U, I0, phitest, n, D, Ntest, r, Q, S, fhat, st);
+  }
   return launch_pred_mfma(w, U, I0, phitest, n, D, Ntest, r, Q, S, fhat, st, timing);
 }
 

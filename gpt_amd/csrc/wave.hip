@@ -184,6 +184,9 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
     for (int i = 0; i < NN; ++i) cs += fabs(S0[i * NN + lc]);
     if (lane >= NN) cs = 0.0;
   }
+  // a non-finite ‖A‖₁ (an Inf or NaN entry): the oracle's NaN result (Julia's expm! would throw at
+  // ceil(Int, log2(nA/5.4))), i.e. geod's bail-out; wave_max (fmax) alone would drop a NaN column
+  if (__any(!(cs <= 1.79769313486231570e308))) return true;
   const double nA = wave_max(cs);
   int si = 0;
   Blk<NN> U, V;
@@ -229,9 +232,11 @@ __device__ __forceinline__ bool wv_expm(double* S0, double* S1, double* S2, int 
     wave_sync();
     blk_mm<NN>(S0, S2, U, lane);
   } else {
+    // as many squarings as Julia's expm! takes (no cap: a capped scaling leaves ‖A/2^s‖ > 5.4, and
+    // the Padé-13 result then differs from the reference's where a diverging chain is about to bail
+    // out; ‖A‖₁ <= DBL_MAX bounds si by 1022)
     const double s = log2(nA / 5.4);
-    si = (s > 0.0) ? (s < 60.0 ? (int)ceil(s) : 60) : 0;
-    if (!(nA == nA)) si = 0;
+    si = (s > 0.0) ? (int)ceil(s) : 0;
     if (si > 0) {
       const double sc = ldexp(1.0, -si);
       for (int o = lane; o < NN * NN; o += 64) S0[o] *= sc;

@@ -131,6 +131,24 @@ class SGLDSession:
                                            C.byref(st)))
         return (ws, Us, st.value, dg) if diag else (ws, Us, st.value)
 
+    def diagnostics(self, chain):
+        """(diag (1 + D, total_steps), status) of one chain of a session created with diag=True:
+        per step [‖gradw‖, ‖gradU_1‖ … ‖gradU_D‖] (engine-dependent rows; zero past a bail-out)."""
+        dg = np.zeros((1 + self.D, self.total_steps), order="F")
+        st = C.c_int32(0)
+        check(lib().gpt_sgld_session_fetch(self._h, chain, None, None,
+                                           dg.ctypes.data_as(_lib.P_D), C.byref(st)))
+        return dg, st.value
+
+    def bail_step(self, chain):
+        """1-based step at which a bailed-out chain hit the geodesic NaN (GPT_SGLD.jl:422-424):
+        the last step with a gradient norm in the diagnostic rows; 0 for a live chain."""
+        dg, st = self.diagnostics(chain)
+        if st == 0:
+            return 0
+        nz = np.flatnonzero(dg[0])
+        return int(nz[-1]) + 1 if nz.size else 0
+
     def close(self):
         if getattr(self, "_h", None):
             lib().gpt_sgld_session_destroy(self._h)
@@ -172,3 +190,16 @@ def pred_device(w_ptr, U_ptr, I0_dev, phitest, n, D, Ntest, r, Q, S, fhat_out, s
     check(lib().gpt_pred_dev(C.c_void_p(w_ptr), C.c_void_p(U_ptr), C.c_void_p(I0_dev.data_ptr()),
                              C.c_void_p(phitest.data_ptr()), n, D, Ntest, r, Q, S,
                              C.c_void_p(fhat_out.data_ptr()), C.c_void_p(stream) if stream else None))
+
+
+VPHASE_KERNELS = {0: "pred_vphase_pairs_kernel", 1: "pred_vphase_rows_pf_kernel",
+                  2: "pred_vphase_rows_kernel", 3: "pred_vphase_kernel",
+                  4: "pred_kernel (direct, no separate V-phase)"}
+
+
+def pred_last_vphase():
+    """Name of the V-phase kernel the last prediction call on this thread launched
+    (gpt_pred_last_vphase), or None before any call."""
+    k = C.c_int32(-1)
+    check(lib().gpt_pred_last_vphase(C.byref(k)))
+    return VPHASE_KERNELS.get(k.value)

@@ -211,6 +211,10 @@ int gpt_pred_trim_pool(void);
 int gpt_pred_dev_timed(const double* w_dev, const double* U_dev, const int32_t* I0_dev,
                        const double* phitest_dev, int64_t n, int64_t D, int64_t Ntest, int64_t r,
                        int64_t Q, int64_t S, double* fhat_dev, void* hip_stream, double* ms_out);
+/* The V-phase kernel the last gpt_pred* call on this thread launched (measurement, no reference
+ * counterpart): 0 pred_vphase_pairs_kernel, 1 pred_vphase_rows_pf_kernel, 2 pred_vphase_rows_kernel,
+ * 3 pred_vphase_kernel, 4 pred_kernel (the direct path, no separate V-phase); -1 before any call. */
+int gpt_pred_last_vphase(int32_t* kind);
 /* Posterior-mean prediction over S samples + RMSE (GPT_SGLD_p.jl:124-132,
  * kin40kExperiment.jl:80-87): mean_out (Ntest), returns rmse*scale in *rmse_out. */
 int gpt_pred_mean(const double* w_store, const double* U_store, const int32_t* I,
@@ -284,7 +288,8 @@ int gpt_cf_fullw_sideinfo(const double* Rating, int64_t N, int64_t ldr, const do
  * w | U, V through the N x r^2 Kronecker design).  n1 / n2 are size(UserData,1) / size(MovieData,1);
  * ytrainMean / ytrainStd are arguments (the reference reads script globals).  Outputs as
  * gpt_cf_fullw_sideinfo with U_store (n1,r,maxepoch), V_store (n2,r,maxepoch).
- * GPT_ERR_NOT_SPD on a non positive definite precision (Julia's PosDefException). */
+ * GPT_ERR_NOT_SPD on a non positive definite precision (Julia's PosDefException): detected within
+ * two epochs of the failed Cholesky, and every output array is zeroed (the reference returns none). */
 int gpt_cf_fullw_gibbs(const double* Rating, int64_t N, int64_t ldr, int64_t n1, int64_t n2,
                        const double* Ratingtest, int64_t Ntest, int64_t ldt, double signal_var,
                        double sigma_u, double sigma_w, const double* w_init, int64_t r,

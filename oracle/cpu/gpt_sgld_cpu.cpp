@@ -407,10 +407,11 @@ int run_chain(const Cfg& c, const double* phi, const double* y, const int32_t* I
             else v = b < r ? (a - r == b ? 1.0 : 0.0) : Ag[(a - r) + r * (b - r)];
             T[a + (size_t)p * b] = sq * v;
           }
-        bool ok = expm(p, T.data(), E);
+        // :23-26: only E is checked (a NaN in expm(−tA) reaches U and bails out the next step)
+        const bool ok = expm(p, T.data(), E);
         std::vector<double> mA((size_t)r * r);
         for (size_t x = 0; x < mA.size(); ++x) mA[x] = -sq * Ag[x];
-        ok = ok && expm(r, mA.data(), mx);
+        if (ok) (void)expm(r, mA.data(), mx);
         if (!ok) {
           if (w_store) std::memset(w_store, 0, sizeof(double) * Q * nstore);
           if (U_store) std::memset(U_store, 0, sizeof(double) * (size_t)n * r * D * nstore);
@@ -463,12 +464,14 @@ extern "C" {
 // OpenMP threads, one chain per thread at a time.  cfg = {n, D, N, r, Q, m, burnin, maxepoch,
 // store_every, max_steps} as int64 and {epsw, epsU, signal_var, sigma_w} as double.  w_out
 // (Q, nchains), U_out (n·r·D, nchains) final states; w_store / U_store (nullable) chain 0's stores
-// in the reference's layout; status[c]: 0 or 1 (geodesic NaN).  *seconds: wall time of the chain
-// loop; returns the total number of steps taken.
+// in the reference's layout; status[c]: 0 or 1 (geodesic NaN); chain_steps[c] (nullable): the steps
+// chain c took (a bailed chain counts its bail-out step).  *seconds: wall time of the chain loop;
+// returns the total number of steps taken.
 long long gptcpu_regression(const int64_t* icfg, const double* dcfg, const double* phi,
                             const double* y, const int32_t* I, int nchains, const uint64_t* seeds,
                             int threads, double* w_out, double* U_out, double* w_store,
-                            double* U_store, int32_t* status, double* seconds) {
+                            double* U_store, int32_t* status, double* seconds,
+                            int64_t* chain_steps) {
   Cfg c;
   c.n = icfg[0]; c.D = icfg[1]; c.N = icfg[2]; c.r = icfg[3]; c.Q = icfg[4]; c.m = icfg[5];
   c.burnin = icfg[6]; c.maxepoch = icfg[7]; c.store_every = icfg[8]; c.max_steps = icfg[9];
@@ -487,6 +490,7 @@ long long gptcpu_regression(const int64_t* icfg, const double* dcfg, const doubl
                              U_out ? U_out + (size_t)ch * nrD : nullptr, ch == 0 ? w_store : nullptr,
                              ch == 0 ? U_store : nullptr, &st);
     if (status) status[ch] = rc;
+    if (chain_steps) chain_steps[ch] = st;
     total += st;
   }
   *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

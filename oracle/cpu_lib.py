@@ -24,7 +24,7 @@ def lib():
         L.gptcpu_regression.restype = C.c_longlong
         L.gptcpu_regression.argtypes = [C.POINTER(C.c_int64), P_D, P_D, P_D, C.POINTER(C.c_int32),
                                         C.c_int, C.POINTER(C.c_uint64), C.c_int, P_D, P_D, P_D, P_D,
-                                        C.POINTER(C.c_int32), P_D]
+                                        C.POINTER(C.c_int32), P_D, C.POINTER(C.c_int64)]
         L.gptcpu_cf_sgd.restype = C.c_double
         PP_I = C.POINTER(C.POINTER(C.c_int32))
         PP_D = C.POINTER(C.POINTER(C.c_double))
@@ -45,8 +45,8 @@ def _p(a, t=C.c_double):
 def GPTregression_chains(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, seeds,
                          threads=1, sigma_w=1.0, store_every=1, max_steps=0, stores=False):
     """Independent GPTregression chains (one per seed) on ``threads`` OpenMP threads.
-    Returns dict(w (Q, C), U (n, r, D, C), status (C,), steps, seconds[, w_store, U_store of
-    chain 0])."""
+    Returns dict(w (Q, C), U (n, r, D, C), status (C,), chain_steps (C,): the steps each chain
+    took, a bail-out step included, steps, seconds[, w_store, U_store of chain 0])."""
     phi = np.asfortranarray(phi, dtype=np.float64)
     n, D, N = phi.shape
     y = np.ascontiguousarray(np.ravel(y), dtype=np.float64)
@@ -62,13 +62,15 @@ def GPTregression_chains(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, max
     ws = np.zeros((Q, T), order="F") if stores else None
     Us = np.zeros((n, r, D, T), order="F") if stores else None
     st = np.zeros(nch, dtype=np.int32)
+    cs = np.zeros(nch, dtype=np.int64)
     sec = C.c_double(0.0)
     steps = lib().gptcpu_regression(_p(icfg, C.c_int64), _p(dcfg), _p(phi), _p(y), _p(I, C.c_int32),
                                     nch, _p(seeds, C.c_uint64), int(threads), _p(w), _p(U), _p(ws),
-                                    _p(Us), _p(st, C.c_int32), C.byref(sec))
+                                    _p(Us), _p(st, C.c_int32), C.byref(sec),
+                                    _p(cs, C.c_int64))
     if steps < 0:
         raise ValueError("gptcpu_regression: unsupported configuration")
-    out = dict(w=w, U=U, status=st, steps=int(steps), seconds=sec.value)
+    out = dict(w=w, U=U, status=st, chain_steps=cs, steps=int(steps), seconds=sec.value)
     if stores:
         out.update(w_store=ws, U_store=Us)
     return out

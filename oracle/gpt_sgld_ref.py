@@ -335,8 +335,8 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
     ``store_every`` = 1 is the reference (a sample after every post-burn-in step);
     ``store_every`` = numbatches keeps the epoch-end samples the scripts consume
     (kin40kExperiment.jl:79).  ``max_steps`` truncates the run (for parity tests).
-    ``info`` holds the status (0 ok, 1 NaN in geodesic) and, with ``record``,
-    per-step gradient norms and fhat.
+    ``info`` holds the status (0 ok, 1 NaN in geodesic; then bail_step, the 1-based step) and,
+    with ``record``, per-step gradient norms and fhat.
     """
     phi = np.asarray(phi, dtype=np.float64)
     y = np.asarray(y, dtype=np.float64).ravel()
@@ -378,6 +378,7 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
                     Un, ok = geod(U[:, :, k], mom, math.sqrt(epsU))
                     if not ok:
                         info["status"] = 1
+                        info["bail_step"] = step + 1          # 1-based step of the bail-out
                         return np.zeros_like(w_store), np.zeros_like(U_store), info
                     U[:, :, k] = Un
             else:

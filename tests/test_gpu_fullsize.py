@@ -117,6 +117,38 @@ def test_fullsize_chain_matches_oracle_and_single_runs(problem):
     s.close()
 
 
+def test_fullsize_chain_long_horizon_matches_oracle(problem):
+    """Long-horizon state parity of the benchmark's launch: chains 0, 97 and 255 of the 256-chain
+    chain-engine session after 1 000 steps (five epochs, four epoch shuffles of the composed order)
+    against the C++ restatement of GPTregression (oracle/cpu/gpt_sgld_cpu.cpp, GPT_SGLD.jl:345-448,
+    same Philox streams) on the same seeds: w and U within 1e-8 (round 6 measured 2.7e-15 after
+    200 steps and 4.7e-14 after 1 000, profiles/r6a_bail_probe.json)."""
+    import torch
+    from gpt_amd.session import SGLDSession
+    from oracle import cpu_lib
+    K, probe = 1000, [0, 97, 255]
+    nb = -(-problem["ytr"].size // m)
+    s = SGLDSession(problem["phi"], problem["y"], problem["I"], r, Q, m, EPSW, EPSU, SV, 0,
+                    -(-K // nb), list(range(1, 257)), store=False, engine="chain")
+    s.run(K)
+    s.sync()
+    w_all = torch.empty((256, Q), dtype=torch.float64, device="cuda")
+    U_all = torch.empty((256, n * r * D), dtype=torch.float64, device="cuda")
+    s.gather_state(0, 256, w_all, U_all)
+    s.sync()
+    assert all(s.status(c) == 0 for c in probe)
+    s.close()
+    wn, Un = w_all.cpu().numpy(), U_all.cpu().numpy()
+    phi_np = np.asfortranarray(problem["phi"].cpu().numpy().transpose(2, 1, 0))
+    o = cpu_lib.GPTregression_chains(phi_np, problem["ytr"], SV, problem["I"], r, Q, m, EPSW, EPSU,
+                                     0, -(-K // nb), np.array([c + 1 for c in probe], dtype=np.uint64),
+                                     threads=3, max_steps=K)
+    assert list(o["chain_steps"]) == [K] * len(probe)
+    for i, c in enumerate(probe):
+        assert rel(wn[c], o["w"][:, i]) < 1e-8, (c, rel(wn[c], o["w"][:, i]))
+        assert rel(Un[c], o["U"][..., i].ravel(order="F")) < 1e-8, c
+
+
 def _gram_err(s, C, n_, r_, D_):
     import torch
     w_all = torch.empty((C, Q), dtype=torch.float64, device="cuda")

@@ -76,6 +76,47 @@ def test_fullw_sideinfo_wide_side_information(lang):
     assert np.all(np.abs(got[5] - want[5]) <= 1e-9 * want[5])
 
 
+@pytest.mark.parametrize("m,r,cols", [(200, 4, None), (1100, 1, 1)])
+def test_fullw_sideinfo_lazy_move_wide_batches(m, r, cols):
+    """The lazy SGD move (cf_epoch_kernel domove = 2, the default for SGD on the feature-mask path)
+    past the bitonic-link batch (B <= 128): m = 200 takes the per-pair link walk; m = 1100
+    (> 1024 threads) also loads its batches without the prefetch — its LDS carve fits only at
+    r = 1 with one side-information column per side (the first of ml-100k's).  Against the
+    oracle's dense per-step move, with the launch mode asserted."""
+    from gpt_amd import movielens
+    tr, te, ud, md, mu, sd = problem(3300, 1000)
+    if cols:
+        ud, md = np.ascontiguousarray(ud[:, :cols]), np.ascontiguousarray(md[:, :cols])
+    w0 = np.random.default_rng(5).standard_normal((r, r))
+    args = (tr, ud, md, te, 0.8, 0.1, 1.0, w0, m, 1e-4, 1e-6, 0.5, 0.25, 0.5, 0, 2, 17, mu, sd)
+    got = movielens.GPT_fullw_sideinfo(*args)
+    assert movielens.last_timing()["mode"] == 2
+    want = M.GPT_fullw_sideinfo(*args)
+    for g, w_ in zip(got[:3], want[:3]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    assert np.abs(got[3] - want[3]).max() < 1e-8
+    assert np.all(np.abs(got[5] - want[5]) <= 1e-9 * want[5])
+
+
+def test_fullw_sideinfo_lazy_equals_eager_move(monkeypatch):
+    """The lazy SGD move (m·c^Δ for the rows a batch skips) against the per-step dense move of
+    every row (GPTSGLD_CF_LAZY=0: a batch-phase launch and a row-parallel move launch per step, the
+    reference's order of operations), 2 epochs of the live configuration's shape on 20 000
+    ratings at r = 20: stores within the 1e-8 store tolerance, test RMSE within 1e-9."""
+    from gpt_amd import movielens
+    tr, te, ud, md, mu, sd = problem(20000, 5000)
+    w0 = np.random.default_rng(17).standard_normal((20, 20))
+    args = (tr, ud, md, te, 0.8, 0.1, 1.0, w0, 100, 1e-4, 1e-6, 0.5, 0.25, 0.5, 0, 2, 17, mu, sd)
+    lazy = movielens.GPT_fullw_sideinfo(*args)
+    assert movielens.last_timing()["mode"] == 2
+    monkeypatch.setenv("GPTSGLD_CF_LAZY", "0")
+    eager = movielens.GPT_fullw_sideinfo(*args)
+    assert movielens.last_timing()["mode"] == 0
+    for g, w_ in zip(lazy[:3], eager[:3]):
+        assert rel(g, w_) < 1e-8, rel(g, w_)
+    assert np.all(np.abs(lazy[5] - eager[5]) <= 1e-9 * eager[5])
+
+
 def test_fullw_sideinfo_live_config_full_fold():
     """The live run of :723-730 (r = 15, m = 100, SGD, a/b/c = 0.5/0.25/0.5) for one epoch of
     fold 1 (80 000 ratings), against the oracle."""

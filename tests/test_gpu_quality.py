@@ -69,6 +69,37 @@ def stiefel_errors(sess, chains, n, r, D):
     return out
 
 
+def _numpy_bail_steps(phi, y, sv, I, r, Q, m, epsw, epsU, cpp_steps):
+    """The numpy restatement's (oracle/gpt_sgld_ref.py, GPT_SGLD.jl:345-448 line by line, numpy /
+    LAPACK arithmetic) 1-based bail-out step of each seed the C++ restatement bails out, run a step
+    past the C++ one (0: no bail-out by then)."""
+    import torch
+    if isinstance(phi, torch.Tensor):
+        phi = np.asfortranarray(phi.cpu().numpy().transpose(2, 1, 0))
+    out = {}
+    for seed, st in cpp_steps.items():
+        with np.errstate(all="ignore"):
+            _, _, info = R.GPTregression(phi, y, sv, I, r, Q, m, epsw, epsU, 0, 1, seed,
+                                         max_steps=st + 1)
+        out[seed] = int(info.get("bail_step", 0))
+    return out
+
+
+def _assert_bail_steps(gpu, cpp, npy):
+    """A diverging chain bails out where its geodesic's expm first holds a NaN (GPT_SGLD.jl:23-26).
+    Its steps before that grow ‖t·[A −S; I A]‖₁ to 1e22-1e27, so expm! scales by 2^-70…2^-89 and
+    squares 70-89 times: whether the squarings of a matrix whose exact exponential is bounded end in
+    an overflow (a NaN, that step) or in finite values (U overflows in tmpU instead, and the NaN
+    input bails out the next step) turns on the last bits of the Padé result, i.e. on the order of
+    the floating-point sums.  The two CPU restatements (C++ loops; numpy/LAPACK) differ from each
+    other by one step on some seeds for that reason (round 6: kin40k_ref seeds 1, 3, 19, 20, 21;
+    profiles/r6_bail_steps.json), and the reference's own step would follow its BLAS.  So: the same
+    chains bail out (asserted by the caller), each within one step of both restatements."""
+    assert set(gpu) == set(cpp) == set(npy), (gpu, cpp, npy)
+    for s in gpu:
+        assert abs(gpu[s] - cpp[s]) <= 1 and abs(gpu[s] - npy[s]) <= 1, (s, gpu, cpp, npy)
+
+
 def test_kin40k_reference_configuration_tracks_reference_curve():
     """kin40kExperiment.jl:38-91 over its full 200 epochs (10 sweeps, r = 20, n = 150) against
     testRMSE_kin40k.h5: bands in the assertions below."""
@@ -132,11 +163,15 @@ def test_kin40k_reference_configuration_tracks_reference_curve():
     assert abs(np.median(curves[:, 29]) / ref[29] - 1.0) <= 0.10
     assert np.all(curves[:, 29] < curves[:, 0])                 # every sweep learns
     # converged (kin40kExperiment.jl:74-90; the reference's 200-epoch curve ends at 0.2385, its
-    # last 50 epochs average 0.2448): the median surviving sweep within 10 % of both, and every
-    # surviving sweep's final RMSE within [0.85, 1.2]x the reference's
-    assert abs(np.median(final) / ref[-1] - 1.0) <= 0.10, (np.median(final), ref[-1])
-    assert abs(np.median(last50) / ref[-50:].mean() - 1.0) <= 0.10, np.median(last50)
-    assert np.all(final >= 0.85 * ref[-1]) and np.all(final <= 1.2 * ref[-1]), final
+    # last 50 epochs average 0.2448).  Nothing here was tuned: the step sizes, hyper-parameter
+    # draws and sweep seeds 1..10 are the script's own (:50-51, :67-72).  The band is the spread of
+    # the sweeps themselves: the 8 surviving finals have s.d. 0.0075 (3.1 % of 0.2385; round 5,
+    # gpurun_out/quality_r3.json), so the median's standard error is ≈ 1.25·3.1 %/√8 ≈ 1.4 % and
+    # 3 % is about two of them; measured +0.3 % (final) and −2.4 % (last-50 mean).  Every surviving
+    # sweep's final within ±10 % (three s.d.; measured 0.937-1.030).
+    assert abs(np.median(final) / ref[-1] - 1.0) <= 0.03, (np.median(final), ref[-1])
+    assert abs(np.median(last50) / ref[-50:].mean() - 1.0) <= 0.03, np.median(last50)
+    assert np.all(final >= 0.9 * ref[-1]) and np.all(final <= 1.1 * ref[-1]), final
 
 
 def test_kin40k_bench_shape_converged_quality():
@@ -146,16 +181,21 @@ def test_kin40k_bench_shape_converged_quality():
     kin40k_step_sweep.py, profiles/r5c_kin40k_sweep*.json, other chain seeds): at r = 5 the median
     chain's epoch-200 RMSE sits at 0.344-0.36 for every stable (εw, εU) pair and for n = 150 as
     well as n = 500, while r = 20 at n = 150 reaches 0.238-0.243 at the same pairs (the reference:
-    0.2385) — the gap to the reference is the rank's capacity, not mixing.  Bands: at most one
-    geodesic bail-out (GPT_SGLD.jl:422-424; measured at this pair: 0 of 256 bench chains, 0 of 16
-    sweep chains, 1 of these 32 — about 0.3 %, so two in 32 has probability ≈ 0.5 %); the
-    median surviving chain's epoch-200 value and last-50 curve mean within [0.33, 0.38]; every
-    surviving chain below its own epoch-1 value; the ensemble of the last 50 epoch-end samples of
-    the surviving chains at most 0.30."""
+    0.2385) — the gap to the reference is the rank's capacity, not mixing.
+    Bail-outs (GPT_SGLD.jl:422-424) are pinned to the oracle, not banded: the chains that bail out
+    over the 200 epochs are exactly the ones the C++ restatement (oracle/cpu, same Philox streams)
+    bails out over its first two epochs, each at the same step.  Round 5 first ran this test with
+    `bailed == 0` and it failed on MI355X (seed 5032); round 6 ran all 32 seeds through the
+    restatement for the full 200 epochs (profiles/r6a_bail_probe.json, 76 s on 16 cores): it bails
+    out seed 5032 alone, at its third step (the initial w draw sends |gradw| 2e6 -> 6e11 -> 1e25),
+    exactly as the chain kernel does.  Bands on the survivors: the median chain's epoch-200 value
+    and last-50 curve mean within [0.33, 0.38]; every chain below its own epoch-1 value; the
+    ensemble of the last 50 epoch-end samples of the surviving chains at most 0.30."""
     import torch
     import bench
     from gpt_amd import GPT_SGLD as G
     from gpt_amd.session import SGLDSession, feature_device, pred_device
+    from oracle import cpu_lib
     dev = torch.device("cuda", 0)
     _, D, m, ls, srbf, sv, _, n, r, epsw, epsU = bench.WORKLOADS["kin40k"]
     Q, epochs, chains = 200, 200, 32
@@ -168,19 +208,25 @@ def test_kin40k_bench_shape_converged_quality():
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     phi = feature_device(tt(Xtr.T), tt(np.array(ls)), srbf, scale, tt(Z.T), tt(b.T))
     phite = feature_device(tt(Xte.T), tt(np.array(ls)), srbf, scale, tt(Z.T), tt(b.T))
-    sess = SGLDSession(phi, tt(ytr), I, r, Q, m, epsw, epsU, sv, 0, epochs,
-                       list(range(5001, 5001 + chains)), store_every=nb, store=True,
-                       engine="chain")
+    seeds = list(range(5001, 5001 + chains))
+    sess = SGLDSession(phi, tt(ytr), I, r, Q, m, epsw, epsU, sv, 0, epochs, seeds,
+                       store_every=nb, store=True, engine="chain")
     sess.run(epochs * nb)
     sess.sync()
+    # the oracle's bail-outs over two epochs, and the step each one bails out at
+    phi_np = np.asfortranarray(phi.cpu().numpy().transpose(2, 1, 0))
+    cpu = cpu_lib.GPTregression_chains(phi_np, ytr, sv, I, r, Q, m, epsw, epsU, 0, 2,
+                                       np.array(seeds, dtype=np.uint64), threads=16)
+    want = {seeds[c]: int(cpu["chain_steps"][c]) for c in range(chains) if cpu["status"][c]}
+    np_steps = _numpy_bail_steps(phi_np, ytr, sv, I, r, Q, m, epsw, epsU, want)
     I0 = torch.from_numpy(np.asfortranarray(I - 1).ravel(order="F").astype(np.int32)).to(dev)
     yte_d = tt(yte)
     fh = torch.empty((epochs, Nte), dtype=torch.float64, device=dev)
     fsum = torch.zeros(Nte, dtype=torch.float64, device=dev)
-    curves, bailed = [], 0
+    curves, got = [], []
     for c in range(chains):
         if sess.status(c) != 0:
-            bailed += 1
+            got.append(seeds[c])
             continue
         _, _, ws, Us, ns = sess.device_state(c)
         assert ns == epochs
@@ -189,12 +235,25 @@ def test_kin40k_bench_shape_converged_quality():
         curves.append((ysd * torch.sqrt((err * err).mean(dim=1))).cpu().numpy())
         fsum += fh[-50:].sum(dim=0)
     sess.close()
-    assert bailed <= 1, bailed
+    bailed = len(got)
+    assert sorted(want) == got, (got, want)
+    # the bail-out step on the device: the last step with a gradient norm in the diagnostic rows
+    bad = [c for c in range(chains) if seeds[c] in want]
+    if bad:
+        sd = SGLDSession(phi, tt(ytr), I, r, Q, m, epsw, epsU, sv, 0, 2, [seeds[c] for c in bad],
+                         store=False, diag=True, engine="chain")
+        sd.run(2 * nb)
+        sd.sync()
+        steps = {seeds[c]: sd.bail_step(i) for i, c in enumerate(bad)}
+        sd.close()
+        _assert_bail_steps(steps, want, np_steps)
     curves = np.array(curves)
     fmean = (fsum / (50 * len(curves))).cpu().numpy()
     ens = float(ysd * math.sqrt(np.mean((fmean - yte) ** 2)))
     final, last50 = curves[:, -1], curves[:, -50:].mean(axis=1)
     _record("kin40k_bench_shape", dict(chains=chains, bailed=bailed, epsw=epsw, epsU=epsU,
+                                       bailed_seeds=got, oracle_bail_steps=want,
+                                       numpy_bail_steps=np_steps,
                                        final=final.tolist(),
                                        last50_curve_mean=last50.tolist(), ensemble_rmse=ens,
                                        median_final=float(np.median(final)),
@@ -406,7 +465,10 @@ def test_kin40k_ref_bailouts_match_oracle():
     that bail out in the first two epochs are exactly the ones the oracle's C++ restatement
     (oracle/cpu/gpt_sgld_cpu.cpp, same Philox streams and seeds) bails out — the bail-out rate is
     the reference algorithm's, not the engine's (7 of these 32 seeds at this pair on this data,
-    the rate the bench's 256-chain run shows over 200 epochs: 32 of 256)."""
+    the rate the bench's 256-chain run shows over 200 epochs: 32 of 256), each at the oracle's
+    step; and every surviving chain's w and U after the 400 steps equal the restatement's within
+    1e-8 (round 6 measured at most 4.7e-11 for w and 2.2e-12 for U, profiles/r6a_bail_probe.json).
+    The diagnostic rows (diag = True) only add stores of the gradient norms."""
     import torch
     import bench
     from gpt_amd import GPT_SGLD as G
@@ -425,12 +487,32 @@ def test_kin40k_ref_bailouts_match_oracle():
     dev = torch.device("cuda", 0)
     phi_d = torch.from_numpy(np.ascontiguousarray(np.transpose(phi, (2, 1, 0)))).to(dev)
     y_d = torch.from_numpy(np.ascontiguousarray(ytr)).to(dev)
-    sess = SGLDSession(phi_d, y_d, I, r, Q, m, 1e-4, 1e-7, 0.0476, 0, epochs, seeds, store=False)
+    sess = SGLDSession(phi_d, y_d, I, r, Q, m, 1e-4, 1e-7, 0.0476, 0, epochs, seeds, store=False,
+                       diag=True)
     assert sess.info()["engine"] == "wave"
     sess.run(epochs * sess.numbatches)
     sess.sync()
     got = sorted(s for c, s in enumerate(seeds) if sess.status(c) != 0)
+    steps = {seeds[c]: sess.bail_step(c) for c in range(C) if sess.status(c) != 0}
+    np_steps = _numpy_bail_steps(phi, ytr, 0.0476, I, r, Q, m, 1e-4, 1e-7,
+                                 {seeds[c]: int(cpu["chain_steps"][c]) for c in range(C)
+                                  if cpu["status"][c]})
+    w_all = torch.empty((C, Q), dtype=torch.float64, device=dev)
+    U_all = torch.empty((C, n * r * D), dtype=torch.float64, device=dev)
+    sess.gather_state(0, C, w_all, U_all)
+    sess.sync()
     sess.close()
-    _record("kin40k_ref_bailouts", dict(chains=C, epochs=epochs, gpu=got, oracle=want))
+    wn, Un = w_all.cpu().numpy(), U_all.cpu().numpy()
+    errs = [(rel(wn[c], cpu["w"][:, c]), rel(Un[c], cpu["U"][..., c].ravel(order="F")))
+            for c in range(C) if seeds[c] not in got and cpu["status"][c] == 0]
+    want_steps = {seeds[c]: int(cpu["chain_steps"][c]) for c in range(C) if cpu["status"][c]}
+    _record("kin40k_ref_bailouts", dict(chains=C, epochs=epochs, gpu=got, oracle=want,
+                                        gpu_steps=steps, oracle_steps=want_steps,
+                                        numpy_steps=np_steps,
+                                        max_w_rel=max(e[0] for e in errs),
+                                        max_U_rel=max(e[1] for e in errs)))
     assert len(want) >= 1, "the pair no longer bails out on this data: the test needs new seeds"
     assert got == want, (got, want)
+    _assert_bail_steps(steps, want_steps, np_steps)
+    assert len(errs) == C - len(want)
+    assert max(e[0] for e in errs) <= 1e-8 and max(e[1] for e in errs) <= 1e-8, errs
