@@ -39,7 +39,7 @@ import os
 import numpy as np
 
 from . import _lib
-from ._lib import C, P_D, P_I32, SGLDConfig, check, lib
+from ._lib import C, P_D, P_I32, P_U64, SGLDConfig, check, lib
 
 
 def _f64(a):
@@ -235,6 +235,56 @@ def GPTregression(phi, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, 
     else:
         check(code)
     return (w_store, U_store, dg) if diag else (w_store, U_store)
+
+
+def GPTregression_chains(phis, y, signal_var, I, r, Q, m, epsw, epsU, burnin, maxepoch, seeds,
+                         sigma_w=1.0, store_every=1, max_steps=0, engine=None):
+    """Independent GPTregression chains in one call (gpt_sgld_regression_chains): the
+    ``@parallel for j=1:10`` sweep block of kin40kExperiment.jl:67-74 (``phis`` a list with one
+    phi per chain, each from its own length scales / sigma_RBF) or posterior chains on one phi
+    (``phis`` a single array).  ``epsw``, ``epsU``, ``signal_var``: a scalar or one value per
+    chain.  Returns a list of (w_store, U_store, status) per chain; status 1 = the geodesic NaN
+    bail-out (that chain's stores are zeros, GPT_SGLD.jl:422-424)."""
+    seeds = [int(s) & (2 ** 64 - 1) for s in seeds]
+    nch = len(seeds)
+    if not isinstance(phis, (list, tuple)):
+        phis = [phis] * nch
+    if len(phis) != nch:
+        raise ValueError("one phi per chain, or one shared phi")
+    uniq = {}
+    for p in phis:                                  # one host copy per distinct array
+        if id(p) not in uniq:
+            uniq[id(p)] = _f64(p)
+    ph = [uniq[id(p)] for p in phis]
+    n, D, N = ph[0].shape
+    if any(p.shape != (n, D, N) for p in ph):
+        raise ValueError("every phi must have the same (n, D, N)")
+    y = _f64(np.asarray(y, dtype=np.float64).ravel())
+    if y.size != N:
+        raise ValueError("phi and y disagree on N")
+    I = np.asfortranarray(np.asarray(I, dtype=np.int32))
+    if I.shape != (Q, D):
+        raise ValueError("I must be (Q, D)")
+
+    def per_chain(v):
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(v, dtype=np.float64), (nch,)))
+        return a, _ptr(a)
+    ew, ew_p = per_chain(epsw)
+    eu, eu_p = per_chain(epsU)
+    sv, sv_p = per_chain(signal_var)
+    cfg = make_config(n, D, N, r, Q, m, ew[0], eu[0], sv[0], sigma_w, burnin, maxepoch, 0, True,
+                      True, store_every, max_steps)
+    T = (maxepoch * (-(-N // m))) // store_every
+    ws = [np.zeros((Q, T), order="F") for _ in range(nch)]
+    Us = [np.zeros((n, r, D, T), order="F") for _ in range(nch)]
+    st = np.zeros(nch, dtype=np.int32)
+    arr = lambda xs: (P_D * nch)(*[_ptr(x) for x in xs])
+    sd = np.array(seeds, dtype=np.uint64)
+    with _engine_env(engine):
+        check(lib().gpt_sgld_regression_chains(C.byref(cfg), nch, sd.ctypes.data_as(P_U64),
+                                               arr(ph), arr([y] * nch), _ptr(I, P_I32), ew_p,
+                                               eu_p, sv_p, arr(ws), arr(Us), _ptr(st, P_I32)))
+    return [(ws[c], Us[c], int(st[c])) for c in range(nch)]
 
 
 def GPT_SGLDERM_RMSprop(phi, y, signal_var, I, r, Q, m, epsilon, alpha, burnin, maxepoch,

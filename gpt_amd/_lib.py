@@ -43,6 +43,9 @@ SIGNATURES = {
     "gpt_sgld_init": (C.c_int, [C.POINTER(SGLDConfig), P_D, P_D]),
     "gpt_sgld_regression": (C.c_int, [C.POINTER(SGLDConfig), P_D, P_D, P_I32, P_D, P_D, P_D, P_D,
                                       P_D]),
+    "gpt_sgld_regression_chains": (C.c_int, [C.POINTER(SGLDConfig), C.c_int32, P_U64,
+                                             C.POINTER(P_D), C.POINTER(P_D), P_I32, P_D, P_D, P_D,
+                                             C.POINTER(P_D), C.POINTER(P_D), P_I32]),
     "gpt_sgld_session_create": (C.c_int, [C.POINTER(SGLDConfig), C.c_int32, P_U64,
                                           C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), P_I32,
                                           C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]),

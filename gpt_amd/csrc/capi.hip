@@ -1052,6 +1052,70 @@ extern "C" int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi
   return host_sampler(cfg, phi, y, I, w_init, U_init, w_store, U_store, diag, 0, 0.0, 0.0);
 }
 
+// Independent chains from host arrays through one device session (the chain / wave engines that
+// the device-pointer session API reaches): kin40kExperiment.jl:67-74's sweep block, every sweep
+// its own phi and hyper-parameters, or posterior chains on one phi.  Each distinct phi / y array is
+// copied to the device once (the pointers may repeat).
+extern "C" int gpt_sgld_regression_chains(const gpt_sgld_config* cfg, int32_t nchains,
+                                          const uint64_t* seeds, const double* const* phi,
+                                          const double* const* y, const int32_t* I,
+                                          const double* epsw, const double* epsU,
+                                          const double* signal_var, double* const* w_store,
+                                          double* const* U_store, int32_t* status) {
+  if (!valid_cfg(cfg)) return GPT_ERR_BAD_DIMS;
+  if (nchains < 1 || !seeds || !phi || !y || !I || !status) {
+    set_error("gpt_sgld_regression_chains: null or empty arguments");
+    return GPT_ERR_BAD_DIMS;
+  }
+  const bool stores = w_store || U_store;
+  for (int c = 0; c < nchains; ++c) {
+    if (!phi[c] || !y[c] || (w_store && !w_store[c]) || (U_store && !U_store[c])) {
+      set_error("gpt_sgld_regression_chains: null per-chain pointer");
+      return GPT_ERR_BAD_DIMS;
+    }
+  }
+  const size_t nphi = (size_t)cfg->n * cfg->D * cfg->N;
+  // one device copy per distinct host array
+  std::vector<std::unique_ptr<DevMem>> mem;
+  std::unordered_map<const double*, const double*> dev_of;
+  auto upload = [&](const double* h, size_t count, const double** out) -> int {
+    auto it = dev_of.find(h);
+    if (it != dev_of.end()) { *out = it->second; return GPT_OK; }
+    std::unique_ptr<DevMem> m(new DevMem());
+    HIPCHK(m->alloc(8 * count));
+    HIPCHK(hipMemcpy(m->p, h, 8 * count, hipMemcpyHostToDevice));
+    *out = m->as<double>();
+    dev_of[h] = *out;
+    mem.push_back(std::move(m));
+    return GPT_OK;
+  };
+  std::vector<const double*> dphi(nchains), dy(nchains);
+  for (int c = 0; c < nchains; ++c) {
+    int rc = upload(phi[c], nphi, &dphi[c]);
+    if (rc == GPT_OK) rc = upload(y[c], (size_t)cfg->N, &dy[c]);
+    if (rc != GPT_OK) return rc;
+  }
+  gpt_sgld_session* s = nullptr;
+  int rc = gpt_sgld_session_create(cfg, nchains, seeds, dphi.data(), dy.data(), I, stores ? 1 : 0,
+                                   nullptr, &s);
+  if (rc != GPT_OK) return rc;
+  std::unique_ptr<gpt_sgld_session, void (*)(gpt_sgld_session*)> guard(s, gpt_sgld_session_destroy);
+  if (epsw || epsU || signal_var)
+    for (int c = 0; c < nchains; ++c) {
+      rc = gpt_sgld_session_set_hyper(s, c, epsw ? epsw[c] : cfg->epsw, epsU ? epsU[c] : cfg->epsU,
+                                      signal_var ? signal_var[c] : cfg->signal_var, cfg->sigma_w);
+      if (rc != GPT_OK) return rc;
+    }
+  rc = gpt_sgld_session_run(s, s->total_steps);
+  if (rc != GPT_OK) return rc;
+  for (int c = 0; c < nchains; ++c) {
+    rc = gpt_sgld_session_fetch(s, c, w_store ? w_store[c] : nullptr, U_store ? U_store[c] : nullptr,
+                                nullptr, &status[c]);
+    if (rc != GPT_OK) return rc;
+  }
+  return GPT_OK;
+}
+
 extern "C" int gpt_sgld_rmsprop(const gpt_sgld_config* cfg, double epsilon, double alpha,
                                 const double* phi, const double* y, const int32_t* I,
                                 const double* w_init, const double* U_init, double* w_store,

@@ -91,6 +91,23 @@ int gpt_sgld_regression(const gpt_sgld_config* cfg, const double* phi, const dou
                         const int32_t* I, const double* w_init, const double* U_init,
                         double* w_store, double* U_store, double* diag);
 
+/* Independent GPTregression chains in one call, from host arrays (kin40kExperiment.jl:67-74: the
+ * `@parallel for j=1:10` sweep block, every sweep its own phi from its own length scales and
+ * sigma_RBF; or posterior chains sharing one phi, BASELINE config 4).  It builds a device session
+ * internally, so the multi-chain engines (chain engine r <= 5, wave engine r = 6..20; the grid
+ * engine while nchains·(D+1) workgroups fit the CUs; GPTSGLD_ENGINE overrides) serve a host that
+ * has no device memory of its own (the Julia shim).  phi[c] (n,D,N), y[c] (N): chain c's inputs
+ * (pointers may repeat; each distinct array is copied to the device once).  seeds[c]: param_seed.
+ * epsw / epsU / signal_var: NULL = cfg's value for every chain, else one per chain (sigma_w is
+ * cfg's).  w_store[c] (Q,T), U_store[c] (n,r,D,T), T = maxepoch*numbatches/store_every, as
+ * gpt_sgld_regression (both NULL: no stores).  status[c]: GPT_OK, or GPT_ERR_NAN_GEODESIC with
+ * that chain's stores zero-filled (GPT_SGLD.jl:422-424); the return value is GPT_OK when every
+ * chain ran to its end or bailed out. */
+int gpt_sgld_regression_chains(const gpt_sgld_config* cfg, int32_t nchains, const uint64_t* seeds,
+                               const double* const* phi, const double* const* y, const int32_t* I,
+                               const double* epsw, const double* epsU, const double* signal_var,
+                               double* const* w_store, double* const* U_store, int32_t* status);
+
 /* GPT_SGLDERM_RMSprop(phi,y,signal_var,I,r,Q,m,epsilon,alpha,burnin,maxepoch)
  * GPT_SGLD.jl:1121-1237: per-entry RMSprop step sizes for w, one averaged step per U^(k), w
  * updated before A.  cfg's epsw/epsU/sigma_w are not used (sigma_w = 1 as in the reference);

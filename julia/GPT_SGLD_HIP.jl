@@ -9,7 +9,8 @@
 # exactly as the reference functions allocate and return them.
 module GPT_SGLD_HIP
 
-export datawhitening, feature, featureNotensor, samplenz, GPTregression, GPT_SGLDERM, pred, RMSE,
+export datawhitening, feature, featureNotensor, samplenz, GPTregression, GPTregression_chains,
+       GPT_SGLDERM, pred, RMSE,
        GPNT_SGLD, GPT_SGLDERM_RMSprop, GPT_SGLDERMw, GPTclassification, GPT_GMC, pred_mean_x,
        init_state
 
@@ -123,6 +124,39 @@ function GPTregression(phi::Array{Float64,3}, y::Array{Float64}, signal_var::Rea
     end
     check(rc)
     return w_store, U_store
+end
+
+# The sweep block of kin40kExperiment.jl:67-74 (`@parallel for j=1:10`, one GPTregression per sweep
+# on that sweep's phitrain) as one call: chain j runs on phis[j] with param_seeds[j] (epsw, epsU,
+# signal_var: one value, or one per chain) in one device session (gpt_sgld_regression_chains: the
+# chain engine at r <= 5, the wave engine at kin40k's r = 20).  Returns [(w_store, U_store, status)]
+# per chain; status 1 = the geodesic NaN bail-out (message + zero stores, :422-424).
+function GPTregression_chains(phis::Vector{Array{Float64,3}}, y::Array{Float64}, signal_var,
+                              I::Array{Int32,2}, r::Integer, Q::Integer, m::Integer, epsw, epsU,
+                              burnin::Integer, maxepoch::Integer, param_seeds::Vector{<:Integer};
+                              sigma_w::Real=1.0, store_every::Integer=1)
+    C = length(param_seeds)
+    length(phis) == C || error("one phi per chain")
+    n, D, N = size(phis[1])
+    T = div(maxepoch * cld(N, m), store_every)
+    perchain(v) = v isa Real ? fill(Float64(v), C) : collect(Float64, v)
+    ew, eu, sv = perchain(epsw), perchain(epsU), perchain(signal_var)
+    cfg = Ref(SGLDConfig(n, D, N, r, Q, m, ew[1], eu[1], sv[1], sigma_w, burnin, maxepoch,
+                         UInt64(0), Int32(1), Int32(1), store_every, 0))
+    ws = [zeros(Q, T) for c = 1:C]; Us = [zeros(n, r, D, T) for c = 1:C]
+    yv = vec(y); status = zeros(Int32, C); seeds = UInt64.(param_seeds)
+    GC.@preserve phis yv ws Us begin
+        check(ccall((:gpt_sgld_regression_chains, LIB), Cint,
+                    (Ref{SGLDConfig}, Int32, Ptr{UInt64}, Ptr{Ptr{Float64}}, Ptr{Ptr{Float64}},
+                     Ptr{Int32}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Ptr{Float64}},
+                     Ptr{Ptr{Float64}}, Ptr{Int32}),
+                    cfg, Int32(C), seeds, pointer.(phis), fill(pointer(yv), C), I, ew, eu, sv,
+                    pointer.(ws), pointer.(Us), status))
+    end
+    for c = 1:C
+        status[c] == 1 && println("Get NaN when moving along Geodesic. Try smaller epsU")
+    end
+    return [(ws[c], Us[c], Int(status[c])) for c = 1:C]
 end
 
 # GPT_SGLDERM(phi,y,sigma,I,r,Q,m,epsw,epsU,burnin,maxepoch)  GPT_SGLD_p.jl:146 (σ_w=√(nᴰ/Q))

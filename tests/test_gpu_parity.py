@@ -523,6 +523,66 @@ def test_multichain_session_equals_single_runs(engine):
     s.close()
 
 
+@pytest.mark.parametrize("shape", ["kin40k_ref_sweeps", "bench_chain_engine"])
+def test_regression_chains_equals_session(shape):
+    """gpt_sgld_regression_chains (the host-array multi-chain entry the Julia shim binds for
+    kin40kExperiment.jl:67-74's sweep block) against a device session of the same chains: the
+    stores are bitwise equal.  kin40k_ref_sweeps: the script's shape (n = 150, r = 20, m = 50,
+    εw = 1e-4, εU = 1e-7; the wave engine), ten sweeps, each its own phi from its own length scales
+    and σ_RBF (:68-72), two epochs of epoch-end samples.  bench_chain_engine: the metric's shape
+    (n = 500, r = 5) on the chain engine, four chains on one phi with per-chain εw / εU / σ²."""
+    import torch
+    import bench
+    from gpt_amd import GPT_SGLD as GG
+    from gpt_amd.session import SGLDSession
+    Xtr, ytr, _, _, _ = bench.kin40k(8)
+    D, Q, m = 8, 200, 50
+    nb = -(-ytr.size // m)
+    if shape == "kin40k_ref_sweeps":
+        n, r, engine, C, epochs = 150, 20, None, 10, 2
+        I = GG.samplenz(r, D, Q, 17)
+        Z, b = GG.feature_inputs(n, D, 17)
+        scale = math.sqrt(n / Q ** (1.0 / D))
+        phis = []
+        for j in range(1, C + 1):
+            g = np.random.default_rng(j)
+            ls = np.ones(D) + 0.2 * g.standard_normal(D)
+            phis.append(GG.feature(Xtr, ls, 1 + 0.2 * g.standard_normal(), scale, Z, b))
+        ew, eu, sv = 1e-4, 1e-7, 0.0476
+        hyper = None
+    else:
+        n, r, engine, C, epochs = 500, 5, "chain", 4, 1
+        I = GG.samplenz(r, D, Q, 17)
+        Z, b = GG.feature_inputs(n, D, 17)
+        phis = GG.feature(Xtr, np.array(bench.KIN40K_LS), 1.0420, math.sqrt(n / Q ** (1.0 / D)), Z, b)
+        ew, eu, sv = [1e-5, 2e-5, 1e-5, 5e-6], [1e-8, 1e-8, 2e-8, 5e-9], [0.0476, 0.05, 0.0476, 0.04]
+        hyper = list(zip(ew, eu, sv))
+    seeds = list(range(1, C + 1))
+    got = GG.GPTregression_chains(phis, ytr, sv, I, r, Q, m, ew, eu, 0, epochs, seeds,
+                                  store_every=nb, engine=engine)
+    plist = phis if isinstance(phis, list) else [phis]
+    dphi = [torch.from_numpy(np.ascontiguousarray(np.transpose(p, (2, 1, 0)))).cuda() for p in plist]
+    y_d = torch.from_numpy(np.ascontiguousarray(ytr)).cuda()
+    s = SGLDSession(dphi, y_d, I, r, Q, m, ew if hyper is None else ew[0],
+                    eu if hyper is None else eu[0], sv if hyper is None else sv[0], 0, epochs, seeds,
+                    store_every=nb, store=True, engine=engine or "auto")
+    assert s.info()["engine"] == ("wave" if engine is None else engine)
+    if hyper:
+        for c, (a, bb, v) in enumerate(hyper):
+            s.set_hyper(c, a, bb, v)
+    s.run(epochs * nb)
+    s.sync()
+    alive = 0
+    for c in range(C):
+        ws, Us, st = s.fetch(c)
+        gw, gU, gst = got[c]
+        assert gst == st, (c, gst, st)
+        assert np.array_equal(gw, ws) and np.array_equal(gU, Us), c
+        alive += st == 0
+    s.close()
+    assert alive >= C // 2
+
+
 @pytest.mark.parametrize("engine", ["grid", "chain", "wave"])
 def test_epoch_order_ring_over_many_epochs(engine):
     """Seven epochs of a ragged N (nb = 4) with every epoch-end sample stored: the two-slot order

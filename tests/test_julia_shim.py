@@ -182,6 +182,7 @@ def test_integration_entry_points_have_julia_bindings():
 
 @pytest.mark.parametrize("sym", ["gpt_cf_fixw", "gpt_cf_fullw", "gpt_cf_fixw_sideinfo",
                                  "gpt_cf_fixw_gibbs", "gpt_cf_fullw_sideinfo_folds",
-                                 "gpt_feature_inputs", "gpt_pred_mean_x", "gpt_sgld_init"])
+                                 "gpt_feature_inputs", "gpt_pred_mean_x", "gpt_sgld_init",
+                                 "gpt_sgld_regression_chains"])
 def test_round3_bindings_present(sym):
     assert sym in {c[1] for c in all_calls()}
