@@ -386,18 +386,32 @@ def movielens_cpu_baseline(folds, w0, cfg, epochs=12):
     hyper = (w0, U0, V0, cfg["signal_var"], cfg["sigma_u"], cfg["sigma_w"], cfg["m"], cfg["epsw"],
              cfg["epsU"], cfg["a"], cfg["b"], cfg["c"])
     nb = -(-N // cfg["m"])
-    sec1, _ = cpu_lib.cf_sgd_folds([(folds[0][0], folds[0][1])], *args, [perms[:2]], *hyper, threads=1)
     nf = len(folds)
-    sec, _ = cpu_lib.cf_sgd_folds([(f[0], f[1]) for f in folds], *args, [perms] * nf, *hyper,
-                                  threads=nf)
-    return dict(value=nf * epochs * nb / sec, unit="fold-steps/s (%d folds on %d cores)" % (nf, nf),
-                cores=nf, kind="port", single_core_steps_per_s=2 * nb / sec1,
-                sample="oracle/cpu/movielens_cpu.cpp (C++ fp64 restatement of "
-                       "100k_movielensExperiment.jl:409-551, SGD, the reference's dense row "
-                       "moves) on the %d folds, %d epochs = %d minibatch steps per fold plus each "
-                       "epoch's train / test evaluation, one OpenMP thread per fold, in %.1f s; "
-                       "fold 1 alone on 1 core for 2 epochs in %.2f s"
-                       % (nf, epochs, epochs * nb, sec, sec1))
+
+    def leg(lazy, E):
+        sec1, _ = cpu_lib.cf_sgd_folds([(folds[0][0], folds[0][1])], *args, [perms[:2]], *hyper,
+                                       threads=1, lazy=lazy)
+        sec, _ = cpu_lib.cf_sgd_folds([(f[0], f[1]) for f in folds], *args, [perms[:E]] * nf,
+                                      *hyper, threads=nf, lazy=lazy)
+        return nf * E * nb / sec, 2 * nb / sec1, sec, sec1
+    # the GPU's algorithm (the lazy prior-decay move) is the fair baseline; the reference's dense
+    # per-step move of every row beside it
+    v, v1, sec, sec1 = leg(True, epochs)
+    d, d1, dsec, dsec1 = leg(False, epochs)
+    return dict(value=v, unit="fold-steps/s (%d folds on %d cores)" % (nf, nf),
+                cores=nf, kind="port", single_core_steps_per_s=v1,
+                sample="oracle/cpu/movielens_cpu.cpp run_fold_lazy (C++ fp64 restatement of "
+                       "100k_movielensExperiment.jl:409-551, SGD, with the GPU's lazy prior-decay "
+                       "move: rows outside a batch read as M*c^k, the same arithmetic regrouped) on "
+                       "the %d folds, %d epochs = %d minibatch steps per fold plus each epoch's "
+                       "train / test evaluation, one OpenMP thread per fold, in %.1f s; fold 1 alone "
+                       "on 1 core for 2 epochs in %.2f s" % (nf, epochs, epochs * nb, sec, sec1),
+                reference_dense_moves=dict(
+                    value=d, unit="fold-steps/s (%d folds on %d cores)" % (nf, nf),
+                    single_core_steps_per_s=d1,
+                    sample="run_fold: the reference's dense per-step move of every U / V row "
+                           "(:481-507), same folds and epochs, in %.1f s; fold 1 on 1 core for 2 "
+                           "epochs in %.2f s" % (dsec, dsec1)))
 
 
 def movielens_main(args):

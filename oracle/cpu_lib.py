@@ -113,11 +113,13 @@ def _csr(data, base):
 
 
 def cf_sgd_folds(folds, UserData, MovieData, perms, w0, U0, V0, signal_var, sigma_u, sigma_w, m,
-                 epsw, epsU, a, b, c, threads=1):
+                 epsw, epsU, a, b, c, threads=1, lazy=False):
     """GPT_fullw_sideinfo SGD epochs (langevin = stiefel = false) of every fold on ``threads``
     OpenMP threads, from the given state: folds = [(Rating, Ratingtest)] (1-based ids,
     standardised ratings), perms[f] = (epochs, N) 0-based orders, w0 (r, r), U0 / V0 (rows, r)
-    row-major starting states shared by the folds.  Returns (seconds, [(w, U, V, sse (epochs, 2))])."""
+    row-major starting states shared by the folds.  ``lazy``: the GPU's lazy prior-decay move
+    (rows outside a batch read as M·c^Δ) instead of the reference's dense per-step move of every
+    row.  Returns (seconds, [(w, U, V, sse (epochs, 2))])."""
     L = lib()
     nf = len(folds)
     n1, D1 = np.asarray(UserData).shape
@@ -150,7 +152,7 @@ def cf_sgd_folds(folds, UserData, MovieData, perms, w0, U0, V0, signal_var, sigm
             arr[k].append(_p(d[k], t))
     def pp(k, t):
         return (C.POINTER(t) * nf)(*arr[k])
-    icfg = np.array([N, Nt, n1, D1, n2, D2, r, m, epochs], dtype=np.int64)
+    icfg = np.array([N, Nt, n1, D1, n2, D2, r, m, epochs, int(bool(lazy))], dtype=np.int64)
     dcfg = np.array([signal_var, sigma_u, sigma_w, epsw, epsU, a, b, c], dtype=np.float64)
     sec = L.gptcpu_cf_sgd(nf, _p(icfg, C.c_int64), _p(dcfg), _p(uptr, C.c_int32), _p(ufe, C.c_int32),
                           _p(vptr, C.c_int32), _p(vfe, C.c_int32), pp("u", C.c_int32),

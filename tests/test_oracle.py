@@ -390,3 +390,8 @@ def test_movielens_cpp_port_matches_numpy_restatement():
         assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
     pred = M.predict(Rt, U, V, w, *M.side_rows(ud, md), 0.5, 0.25, 0.5)
     assert sse[1, 1] == pytest.approx(np.sum((Rt[:, 2] - pred) ** 2), rel=1e-12)
+    # the lazy prior-decay move (the GPU's one-launch epoch, cf.hip domove = 2): the same numbers
+    _, outs_l = cpu_lib.cf_sgd_folds([(R, Rt)], ud, md, [perms], w0, U0, V0, 0.8, 0.1, 1.0, m,
+                                     1e-3, 1e-3, 0.5, 0.25, 0.5, lazy=True)
+    for got, ref in zip(outs_l[0], outs[0]):
+        assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
