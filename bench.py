@@ -304,6 +304,7 @@ def compose_line(v):
         "test_rmse_note": v.quality["note"],
         "quality": v.quality,
         "allreduce_ms": v.allreduce_ms,
+        "timed_region_host_us": v.host_us,
         "pred": {"samples": v.npred, "Ntest": v.Nte, "ms": v.pred_ms, "gemm_flop": v.pred_flop,
                  "achieved_tflops": pred_tfs, "peak_tflops": FP64_MFMA_PEAK_TFS,
                  "frac": pred_tfs / FP64_MFMA_PEAK_TFS,
@@ -728,19 +729,29 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
+    pc = time.perf_counter
+    t0 = pc()
     ev0.record(tstream)
+    t1 = pc()
     sess.run(args.steps)
+    t2 = pc()
     ev1.record(tstream)
-    sess.sync()
+    t3 = pc()
+    # one device synchronisation closes the region: the session runs on tstream, which it drains
+    # (a separate hipStreamSynchronize first measured 3-83 µs more, scripts/host_overhead.py)
+    t4 = pc()
     torch.cuda.synchronize()
+    t5 = pc()
     if world > 1:
         dist.barrier()
-    dt_rank = time.perf_counter() - t0
+    dt_rank = pc() - t0
+    host_us = {"ev0_record": 1e6 * (t1 - t0), "run_call": 1e6 * (t2 - t1),
+               "ev1_record": 1e6 * (t3 - t2), "device_sync": 1e6 * (t5 - t4)}
     profile_marker(tstream)
     # device time of the timed steps on the session stream (the graph launches of the timed
     # region, gaps between their kernels included): <= the wall time above by construction
     k_us = 1000.0 * ev0.elapsed_time(ev1) / args.steps
+    host_us["wall_minus_event_total"] = 1e6 * dt_rank - 1000.0 * ev0.elapsed_time(ev1)
     # chains that hit the geodesic NaN bail-out (GPT_SGLD.jl:422-424) stop stepping; at the
     # reference's own kin40k configuration (εw = 1e-4, εU = 1e-7) about one chain in eight does,
     # as in the reference, and PowerPlant's εw = 5e-5 / εU = 2e-8 loses a few of 512.  Only the
@@ -916,7 +927,7 @@ def main():
             k_us_ranks=k_us_ranks, bytes_launch=bytes_launch, steps_run=steps_run, cpu=cpu,
             quality=quality, allreduce_ms=allreduce_ms, npred=npred, pred_ms=pred_ms,
             pred_flop=pred_flop, gemm_ms=gemm_ms, vphase_ms=vphase_ms, rmse_final=rmse_final,
-            vphase_kernel=vphase_kernel,
+            vphase_kernel=vphase_kernel, host_us=host_us,
             single=single))
         print(json.dumps(out))
     sess.close()

@@ -98,6 +98,24 @@ struct ChainLds {
 #define CHAIN_STAMPS CHAIN_SSTAMP
 #endif
 #define CHAIN_FENCE() do {} while (0)
+// Post-batch wave priorities.  The two waves of a SIMD (dimensions k and k + 4) run the same
+// per-wave Stiefel phase after the batch; with equal priority the older wave runs ahead and its
+// partner finishes the phase alone, every latency exposed.  Waves k >= 4 take priority 1 for the
+// w update and the U noise, waves k < 4 from the projection through the 2r × 2r expm, waves
+// k >= 4 again from expm(−tA) to the end of the step: 201.0 k → 196.8 k shader cycles per 256-chain
+// step (−2.1 %, two alternating A/B rounds, profiles/r6_chain_priority_ab.txt); a fixed priority
+// (+1 %), a flip at every sub-phase (+4 %) and other flip points (−0.1 … −1.2 %) measured worse.
+// CHAIN_PRIO=0 builds the equal-priority kernel for comparison.
+#ifndef CHAIN_PRIO
+#define CHAIN_PRIO 2
+#endif
+#define CHAIN_SETPRIO(hi_upper)                                                             \
+  do {                                                                                      \
+    if (CHAIN_PRIO) {                                                                       \
+      if ((k >= 4) == (hi_upper)) __builtin_amdgcn_s_setprio(1);                            \
+      else __builtin_amdgcn_s_setprio(0);                                                   \
+    }                                                                                       \
+  } while (0)
 #if !CHAIN_STAMPS
 #define CSTAMP(slot) CHAIN_FENCE()
 #endif
@@ -147,6 +165,8 @@ struct ChainLds {
 // stamp row (2 + i/8)·gridDim.x + blockIdx.x (columns i%8, +8 for wave 4).
 #define SSTAMP(slot)                                                                        \
   do {                                                                                      \
+    if ((slot) == 4) CHAIN_SETPRIO(false);  /* after the U noise: waves k < 4 first */      \
+    if ((slot) == 7) CHAIN_SETPRIO(true);   /* after the 2r x 2r expm: waves k >= 4 */     \
     if (CHAIN_SSTAMP && P.stamps && lane == 0 && (k == 0 || k == 4))                                        \
       P.stamps[(size_t)((2 + (slot) / 8) * gridDim.x + blockIdx.x) * kStamps + (k ? 8 : 0) + \
                (slot) % 8] = (long long)__builtin_amdgcn_s_memtime();                       \
@@ -491,6 +511,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
   SSTAMP(0);
   __syncthreads();
   SSTAMP(1);
+  CHAIN_SETPRIO(true);
   {
     const double inv_sw2 = 1.0 / (C.sigma_w * C.sigma_w);
     const double sqe = sqrt(C.epsw);
@@ -736,6 +757,7 @@ __global__ __launch_bounds__(64 * WV, WV == 4 ? 2 : 1) void chain_kernel(StepPar
       }
     }
     SSTAMP(13);
+    if (CHAIN_PRIO) __builtin_amdgcn_s_setprio(0);
     if (CHAIN_STAMPS && P.stamps && lane == 0)   // per-wave arrival at the end-of-step barrier
     P.stamps[(size_t)blockIdx.x * kStamps + 8 + k] = (long long)__builtin_amdgcn_s_memtime();
   __syncthreads();                      // w_l, flag and the gradw partials are complete

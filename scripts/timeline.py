@@ -45,7 +45,10 @@ def analyse(tl, nsteps, ev_us, tag):
         sel = xcc == x
         per_xcc[int(x)] = dict(chains=int(sel.sum()), mean_end_us=float(last[sel].mean()),
                                max_end_us=float(last[sel].max()),
-                               mean_step_us=float(step[sel].mean()))
+                               mean_step_us=float(step[sel].mean()),
+                               clock_mhz_median=float(np.median(mhz[sel])),
+                               cycles_per_step_median=float(np.median(np.diff(mt[sel][:, 1:], axis=1))),
+                               prologue_us_mean=float((pro - entry)[sel].mean()))
     out = dict(
         tag=tag, steps=nsteps, chains=C_, event_us=ev_us,
         event_us_per_step=ev_us / nsteps,

@@ -123,7 +123,7 @@ def test_bench_line_fields_at_world_2():
                   steps_run=41000, cpu=dict(value=17000.0, cores=16, kind="port"),
                   quality=quality, allreduce_ms=0.05, npred=256, pred_ms=6.9, pred_flop=3.07e11,
                   gemm_ms=5.4, vphase_ms=1.0, rmse_final=0.28,
-                  vphase_kernel="pred_vphase_pairs_kernel",
+                  vphase_kernel="pred_vphase_pairs_kernel", host_us={},
                   single=dict(steps_per_s=2e4, kernel_us=50.0))
     one = bench.compose_line(types.SimpleNamespace(world=1, world_seen=1, k_us=93.0,
                                                    k_us_ranks=[93.0], **common))
