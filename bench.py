@@ -605,7 +605,7 @@ def main():
     ap.add_argument("--epsU", type=float, default=None, help="default: the workload's")
     ap.add_argument("--signal_var", type=float, default=None, help="default: the workload's")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--clock-warm-ms", type=float, default=300.0,
+    ap.add_argument("--clock-warm-ms", type=float, default=1000.0,
                     help="untimed GPU clock warm-up on a scratch session before the warmup steps")
     ap.add_argument("--epochs", type=int, default=200,
                     help="epochs every chain runs in total (kin40kExperiment.jl:74: maxepoch 200); "

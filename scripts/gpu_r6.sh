@@ -30,6 +30,7 @@ for s in "$@"; do
     driver)   for i in 1 2 3; do run driver$i 200 $DF; done ;;
     driver1)  run driver1 200 $DF ;;
     quick)    for i in 1 2 3; do run quick$i 200 $DF --no-cpu-baseline --no-single-chain; done ;;
+    warmab)   for i in 1 2 3; do run wa1000_$i 200 $DF --no-cpu-baseline --no-single-chain --clock-warm-ms 1000; run wa2500_$i 200 $DF --no-cpu-baseline --no-single-chain --clock-warm-ms 2500; done ;;
     long)     run long 300 python -u bench.py --steps 2000 --warmup 200 --no-cpu-baseline ;;
     profdf)   run profdf 300 $RP -d gpurun_out/${T}_prof_df -o run -- $DF --no-cpu-baseline --no-single-chain; squeeze df ;;
     ref)      run ref 400 python -u bench.py --workload kin40k_ref --no-cpu-baseline ;;
