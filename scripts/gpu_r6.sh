@@ -43,6 +43,8 @@ for s in "$@"; do
     hostspin) run hostspin 300 python -u scripts/host_overhead.py --spin-flags --out gpurun_out/${T}_hostspin.json ;;
     hostaw)   run hostaw 300 env ROC_ACTIVE_WAIT_TIMEOUT=200 python -u scripts/host_overhead.py --out gpurun_out/${T}_hostaw.json ;;
     stamps)   run stamps 300 env GPTSGLD_LIB=gpt_amd/libgptsgld_diag.so python -u scripts/phase_stamps.py --engine chain --chains 256 --steps 30 ;;
+    round)    run round 900 env TAG=${T} bash scripts/profile_round.sh --steps 20 --warmup 5 ;;
+    pmc)      run pmc 900 env TAG=${T} bash scripts/pmc_chain.sh ;;
     smoke)    run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *)        echo "unknown step $s"; exit 2 ;;
   esac
