@@ -45,6 +45,7 @@ for s in "$@"; do
     stamps)   run stamps 300 env GPTSGLD_LIB=gpt_amd/libgptsgld_diag.so python -u scripts/phase_stamps.py --engine chain --chains 256 --steps 30 ;;
     round)    run round 900 env TAG=${T} bash scripts/profile_round.sh --steps 20 --warmup 5 ;;
     pmc)      run pmc 900 env TAG=${T} bash scripts/pmc_chain.sh ;;
+    single)   run single 300 python -u scripts/single_chain_ab.py ;;
     smoke)    run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *)        echo "unknown step $s"; exit 2 ;;
   esac
