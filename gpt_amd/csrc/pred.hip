@@ -328,36 +328,6 @@ __global__ __launch_bounds__(256) void pred_temp_mfma_kernel(const double* __res
       }
 }
 
-// fhat[s·Ntest + i] = Σ_q w_s[q] Π_k T[(s·D + k)·R + I[q,k]][i] for a 64-row tile of sample s.
-template <int R>
-__global__ __launch_bounds__(kNT) void pred_vphase_kernel(const double* __restrict__ w,
-                                                          const double* __restrict__ T,
-                                                          const int32_t* __restrict__ I0, int D,
-                                                          long long Ntest, int Q,
-                                                          double* __restrict__ fhat) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int MP = 65;
-  size_t o = 0;
-  double* temp_l = (double*)(smem + o); o = al16(o + 8 * (size_t)D * R * MP);
-  int* I_l = (int*)(smem + o);          o = al16(o + 4 * (size_t)Q * D);
-  double* w_l = (double*)(smem + o);
-  const int tid = threadIdx.x;
-  const int s = blockIdx.y;
-  const long long i0 = (long long)blockIdx.x * 64;
-  const int Bt = (int)min((long long)64, Ntest - i0);
-  for (int x = tid; x < Q * D; x += kNT) I_l[x] = I0[x];
-  for (int q = tid; q < Q; q += kNT) w_l[q] = w[(size_t)s * Q + q];
-  const double* Ts = T + ((size_t)s * ((Ntest + 63) / 64) + blockIdx.x) * D * R * 64;
-  for (int x = tid; x < D * R * 64; x += kNT) {
-    const int row = x >> 6, i = x & 63;
-    if (i < Bt) temp_l[row * MP + i] = gptr(Ts)[(size_t)row * 64 + i];
-  }
-  __syncthreads();
-  vphase_tile<R, VCfg<R>::ICV_MAX>(temp_l, MP, I_l, w_l, Q, D, 0, Bt, [&](int comp, int i, double v) {
-    if (comp == 0) fhat[(size_t)s * Ntest + i0 + i] = v;
-  });
-}
-
 // V-phase over the stacked temp with lanes as test rows: one wave = (sample s, 64 rows); the
 // wave stages its D·R temp rows (64 doubles each, coalesced) into LDS, then for every core entry q
 // the D factors temp[k, I[q,k]] are lane-contiguous LDS reads (no bank conflicts) at offsets the
@@ -637,13 +607,8 @@ __global__ __launch_bounds__(64 * kPairWaves) void pred_vphase_pairs_kernel(
   }
 }
 
-static size_t pred_vphase_lds_bytes(int D, int r, int Q) {
-  return al16(8 * (size_t)D * r * 65) + al16(4 * (size_t)Q * D) + al16(8 * (size_t)Q);
-}
 
-
-// Workgroup tile of the stacked-sample GEMM: GPTSGLD_PRED_TILE = "22" (64 × 64, default "44")
-// selects the wave tile (16·TM c × 16·TN i) for comparison runs.
+// Workgroup tile of the stacked-sample GEMM: a wave tile of 16·TM c × 16·TN i (TM = TN = 4).
 template <int TM, int TN>
 static void launch_pred_gemm_t(const double* Us, const double* phitest, int n, int D, int r,
                                long long Ntest, int Sc, double* T, hipStream_t st,
@@ -663,12 +628,8 @@ static hipError_t launch_pred_gemm(const double* Us, const double* phitest, int 
                                    long long Ntest, int Sc, double* T, hipStream_t st,
                                    long long nti64 = -1) {
   if (nti64 < 0) nti64 = (Ntest + 63) / 64;
-  const char* ev = std::getenv("GPTSGLD_PRED_TILE");
-  const int tile = ev ? std::atoi(ev) : 44;
-  if (tile == 22) launch_pred_gemm_t<2, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st, nti64);
-  else if (tile == 42) launch_pred_gemm_t<4, 2>(Us, phitest, n, D, r, Ntest, Sc, T, st, nti64);
-  else if (tile == 24) launch_pred_gemm_t<2, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st, nti64);
-  else launch_pred_gemm_t<4, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st, nti64);
+  // 4 × 4 MFMA tiles per wave (the 2 × 2, 4 × 2 and 2 × 4 variants measured slower, round 3)
+  launch_pred_gemm_t<4, 4>(Us, phitest, n, D, r, Ntest, Sc, T, st, nti64);
   return hipGetLastError();
 }
 
@@ -698,13 +659,13 @@ static hipError_t vphase_pairs(int NTp, const double* w, const double* T, const 
 
 // Which V-phase kernel the last prediction call on this thread launched (gpt_pred_last_vphase):
 // 0 pred_vphase_pairs_kernel, 1 pred_vphase_rows_pf_kernel, 2 pred_vphase_rows_kernel,
-// 3 pred_vphase_kernel (tile), 4 pred_kernel (direct, no separate V-phase).
+// 4 pred_kernel (direct, no separate V-phase).
 static thread_local int g_pred_vphase = -1;
 int pred_last_vphase() { return g_pred_vphase; }
 
-// The rows V-phase: the persistent prefetching kernel while a tile's D·R rows fit 16 per wave
-// (GPTSGLD_PRED_ROWS_PF=0: the one-tile-per-workgroup kernel, for comparison), as many workgroups
-// as the LDS lets every CU hold.
+// The rows V-phase: the persistent prefetching kernel while a tile's D·R rows fit 16 per wave and
+// its LDS fits a CU (as many workgroups as the LDS lets every CU hold), else the
+// one-tile-per-workgroup kernel.
 constexpr int kRowsPfWaves = 16;
 template <int DD, int NPW, int NW = kRowsPfWaves>
 static hipError_t launch_rows_pf(const double* w, const double* T, const int32_t* offs, int D, int r,
@@ -731,15 +692,11 @@ static hipError_t launch_rows_pf(const double* w, const double* T, const int32_t
 static hipError_t launch_vphase_rows(const double* w, const double* T, const int32_t* offs, int D,
                                      int r, long long Ntest, int Q, double* fhat, int Sc,
                                      size_t rlds, hipStream_t st) {
-  static const bool pf = [] {
-    const char* ev = std::getenv("GPTSGLD_PRED_ROWS_PF");
-    return !(ev && std::strcmp(ev, "0") == 0);
-  }();
   // (the persistent kernel's LDS: the tile's rows, the wave partials, the entries' offsets and
   // the sample's w — a large core (Q·D) can push it past one CU's 160 KB)
   const size_t pf_lds = 8 * (size_t)D * r * 64 + 8 * (size_t)kRowsPfWaves * 64 +
                         4 * (((size_t)Q * D + 3) & ~(size_t)3) + 8 * (size_t)Q;
-  if (pf && D * r <= kRowsPfWaves * 16 && pf_lds <= 160 * 1024) {
+  if (D * r <= kRowsPfWaves * 16 && pf_lds <= 160 * 1024) {
     // rows per wave: 10 (D·r ≤ 160: kin40kExperiment.jl's D = 8, r = 20) or 16
     if (D * r <= kRowsPfWaves * 10) {
       switch (D) {
@@ -828,12 +785,6 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
     unit = 128 / g;
     if (chunk < S && chunk >= unit) chunk = chunk / unit * unit;
   }
-  // GPTSGLD_PRED_ALLOC=plain: hipMalloc / hipFree around the call instead of the private pool
-  // (diagnostic: page-size / TLB behaviour of the pass buffer)
-  static const bool plain_alloc = [] {
-    const char* ev = std::getenv("GPTSGLD_PRED_ALLOC");
-    return ev && std::strcmp(ev, "plain") == 0;
-  }();
   hipMemPool_t pool = nullptr;
   hipError_t e = pred_pool(&pool);
   if (e != hipSuccess) return e;
@@ -842,13 +793,8 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
   size_t tbytes = 0;
   for (;;) {          // out of device memory: halve the pass (whole 128-column tiles while it can)
     tbytes = (per_sample * chunk + 255) / 256 * 256;
-    if (plain_alloc) {
-      e = hipStreamSynchronize(st);
-      if (e == hipSuccess) e = hipMalloc((void**)&T, tbytes + 4 * (size_t)Q * D + 4 * (size_t)Q * NTp);
-    } else {
-      e = hipMallocFromPoolAsync((void**)&T, tbytes + 4 * (size_t)Q * D + 4 * (size_t)Q * NTp, pool,
-                                 st);
-    }
+    e = hipMallocFromPoolAsync((void**)&T, tbytes + 4 * (size_t)Q * D + 4 * (size_t)Q * NTp, pool,
+                               st);
     if (e != hipErrorOutOfMemory || chunk == 1) break;
     (void)hipGetLastError();
     chunk = chunk / 2 >= unit ? chunk / 2 / unit * unit : std::max(1, chunk / 2);
@@ -857,17 +803,14 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
   int32_t* offs = (int32_t*)((char*)T + tbytes);
   int32_t* offp = offs + (size_t)Q * D;
   const size_t rlds = 8 * (size_t)D * r * 64 + 8 * (size_t)kRowsWaves * 64;
-  // V-phase variant: "pairs" (default where the tables fit: ⌈D/2⌉ ≤ 8 and ≤ 96 KB), "rows", "tile"
+  // V-phase variant: "pairs" (default where the tables fit: ⌈D/2⌉ ≤ 8 and ≤ 96 KB), else "rows";
+  // GPTSGLD_PRED_VPHASE=rows forces the rows form (tests/test_gpu_parity.py compares the two)
   const int vmode = [] {
     const char* ev = std::getenv("GPTSGLD_PRED_VPHASE");
-    if (ev && std::strcmp(ev, "tile") == 0) return 2;
-    if (ev && std::strcmp(ev, "rows") == 0) return 1;
-    return 0;
+    return (ev && std::strcmp(ev, "rows") == 0) ? 1 : 0;
   }();
   const size_t plds = pred_pairs_lds_bytes(D, r);
   const bool pairs = vmode == 0 && r <= 5 && NTp <= 8 && plds <= 96 * 1024;
-  const bool tile_vphase = vmode == 2;
-  const size_t vlds = pred_vphase_lds_bytes(D, r, Q);
   for (int s0 = 0; s0 < S && e == hipSuccess; s0 += chunk) {
     const int Sc = std::min(chunk, S - s0);
     const double* Us = U + (size_t)s0 * n * r * D;
@@ -880,12 +823,11 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
       if (pairs)
         hipLaunchKernelGGL(pred_pair_offs_kernel, dim3((Q * NTp + 255) / 256), dim3(256), 0, st, I0,
                            Q, D, r, offp);
-      else if (!tile_vphase)
+      else
         hipLaunchKernelGGL(pred_offs_kernel, dim3((Q * D + 255) / 256), dim3(256), 0, st, I0, Q, D,
                            r, offs);
     }
     if (timing) (void)hipEventRecord(ev[1], st);
-    dim3 vg((unsigned)((Ntest + 63) / 64), Sc);
     if (pairs) {
       g_pred_vphase = 0;
       e = vphase_pairs(NTp, w + (size_t)s0 * Q, T, offp, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest,
@@ -901,43 +843,19 @@ static hipError_t launch_pred_mfma(const double* w, const double* U, const int32
       }
       continue;
     }
-    if (!tile_vphase) {
-      e = launch_vphase_rows(w + (size_t)s0 * Q, T, offs, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest,
-                             Sc, rlds, st);
-      if (timing && e == hipSuccess) {
-        (void)hipEventRecord(ev[2], st);
-        (void)hipEventSynchronize(ev[2]);
-        float a = 0.f, b = 0.f;
-        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
-        (void)hipEventElapsedTime(&b, ev[1], ev[2]);
-        timing->gemm_ms += a;
-        timing->vphase_ms += b;
-      }
-      continue;
-    }
-    g_pred_vphase = 3;
-    switch (r) {
-#define CASE(RR)                                                                             \
-  case RR: {                                                                                 \
-    static std::atomic<uint64_t> attr{0};                                                         \
-    e = set_max_lds_once((const void*)pred_vphase_kernel<RR>, 160 * 1024, attr);                  \
-    if (e != hipSuccess) break;                                                                   \
-    hipLaunchKernelGGL(pred_vphase_kernel<RR>, vg, dim3(kNT), vlds, st, w + (size_t)s0 * Q, T, \
-                       I0, D, Ntest, Q, fhat + (size_t)s0 * Ntest);                          \
-    e = hipGetLastError();                                                                   \
-  } break;
-      GPT_RANKS(CASE)
-#undef CASE
-      default: e = hipErrorInvalidValue;
+    e = launch_vphase_rows(w + (size_t)s0 * Q, T, offs, D, r, Ntest, Q, fhat + (size_t)s0 * Ntest,
+                           Sc, rlds, st);
+    if (timing && e == hipSuccess) {
+      (void)hipEventRecord(ev[2], st);
+      (void)hipEventSynchronize(ev[2]);
+      float a = 0.f, b = 0.f;
+      (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+      (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+      timing->gemm_ms += a;
+      timing->vphase_ms += b;
     }
   }
-  hipError_t ef = hipSuccess;
-  if (plain_alloc) {
-    ef = hipStreamSynchronize(st);
-    if (ef == hipSuccess) ef = hipFree(T);
-  } else {
-    ef = hipFreeAsync(T, st);
-  }
+  const hipError_t ef = hipFreeAsync(T, st);
   return e != hipSuccess ? e : ef;
 }
 

@@ -193,8 +193,7 @@ def pred_device(w_ptr, U_ptr, I0_dev, phitest, n, D, Ntest, r, Q, S, fhat_out, s
 
 
 VPHASE_KERNELS = {0: "pred_vphase_pairs_kernel", 1: "pred_vphase_rows_pf_kernel",
-                  2: "pred_vphase_rows_kernel", 3: "pred_vphase_kernel",
-                  4: "pred_kernel (direct, no separate V-phase)"}
+                  2: "pred_vphase_rows_kernel", 4: "pred_kernel (direct, no separate V-phase)"}
 
 
 def pred_last_vphase():

@@ -230,7 +230,7 @@ int gpt_pred_dev_timed(const double* w_dev, const double* U_dev, const int32_t* 
                        int64_t Q, int64_t S, double* fhat_dev, void* hip_stream, double* ms_out);
 /* The V-phase kernel the last gpt_pred* call on this thread launched (measurement, no reference
  * counterpart): 0 pred_vphase_pairs_kernel, 1 pred_vphase_rows_pf_kernel, 2 pred_vphase_rows_kernel,
- * 3 pred_vphase_kernel, 4 pred_kernel (the direct path, no separate V-phase); -1 before any call. */
+ * 4 pred_kernel (the direct path, no separate V-phase); -1 before any call. */
 int gpt_pred_last_vphase(int32_t* kind);
 /* Posterior-mean prediction over S samples + RMSE (GPT_SGLD_p.jl:124-132,
  * kin40kExperiment.jl:80-87): mean_out (Ntest), returns rmse*scale in *rmse_out. */

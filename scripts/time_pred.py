@@ -1,8 +1,9 @@
-"""Time the stacked-sample prediction (MFMA GEMM + V-phase) per GEMM wave tile on the GPU.
+"""Time the stacked-sample prediction (MFMA GEMM + V-phase) on the GPU.
 
     python scripts/time_pred.py [--S 256] [--n 500] [--r 5] [--Ntest 30000]
-Prints ms per call and the GEMM's fp64 TFLOP/s for each GPTSGLD_PRED_TILE (22, 42, 24, 44) and
-GPTSGLD_PRED_VPHASE (pairs, rows, tile) combination asked for.
+Prints ms per call and the GEMM's fp64 TFLOP/s for each GPTSGLD_PRED_VPHASE (pairs, rows) asked
+for.  (Rounds 3-5 also compared GEMM wave tiles and a tile V-phase; those switches were removed
+from the library in round 6 with the 4 x 4 tile kept.)
 """
 import argparse
 import os
@@ -23,9 +24,8 @@ def main():
     ap.add_argument("--Q", type=int, default=200)
     ap.add_argument("--Ntest", type=int, default=30000)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--tiles", default="22,42,24,44")
     ap.add_argument("--vphases", default="pairs,rows",
-                    help="GPTSGLD_PRED_VPHASE values to compare (pairs, rows, tile)")
+                    help="GPTSGLD_PRED_VPHASE values to compare (pairs, rows)")
     a = ap.parse_args()
     import torch
     from gpt_amd import GPT_SGLD as G
@@ -40,8 +40,7 @@ def main():
     f = torch.empty(a.S, a.Ntest, dtype=torch.float64, device=dev)
     flop = 2.0 * a.S * a.r * a.n * a.D * a.Ntest
     ref = None
-    for tile, vp in [(t, v) for t in a.tiles.split(",") for v in a.vphases.split(",")]:
-        os.environ["GPTSGLD_PRED_TILE"] = tile
+    for vp in a.vphases.split(","):
         os.environ["GPTSGLD_PRED_VPHASE"] = vp
         pred_device(w.data_ptr(), U.data_ptr(), I0, phi, a.n, a.D, a.Ntest, a.r, a.Q, a.S, f)
         torch.cuda.synchronize()
@@ -55,8 +54,8 @@ def main():
         if ref is None:
             ref = f.clone()
         d = (f - ref).abs().max().item() / ref.abs().max().item()
-        print("tile %s vphase %s: %.3f ms per call (GEMM + V-phase), GEMM flop / call time %.1f "
-              "TFLOP/s, max rel diff vs the first %.1e" % (tile, vp, ms, flop / ms / 1e9, d), flush=True)
+        print("vphase %s: %.3f ms per call (GEMM + V-phase), GEMM flop / call time %.1f "
+              "TFLOP/s, max rel diff vs the first %.1e" % (vp, ms, flop / ms / 1e9, d), flush=True)
 
 
 if __name__ == "__main__":
