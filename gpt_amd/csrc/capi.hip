@@ -1856,6 +1856,9 @@ static int cf_sgd_run(
     HIPCHK(hipMemset(d_stamps.p, 0, 8 * (size_t)kCfStampSteps * kCfStampSlots));
     P.stamps = d_stamps.as<long long>();
   }
+#if CF_WSTAMPS
+  if (std::getenv("GPTSGLD_CF_EXP")) P.exp = std::atoi(std::getenv("GPTSGLD_CF_EXP"));
+#endif
   for (CfFold& fd : folds) {
     if (fd.w_store) std::memset(fd.w_store, 0, 8 * rr * maxepoch);
     std::memset(fd.U_store, 0, 8 * nU * maxepoch);

@@ -29,6 +29,21 @@ typedef double pd4 __attribute__((ext_vector_type(4)));
       P.stamps[(size_t)(bt) * kCfStampSlots + (slot)] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 
+// Per-wave sub-phase stamps (diagnostic builds with CF_WSTAMPS): lane 0 of every wave of chain 0,
+// slots 8 + 4·wave + i of the step's stamp row.
+#if CF_WSTAMPS
+#define CF_WSTAMP(bt, i)                                                                      \
+  do {                                                                                        \
+    if (P.stamps && blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (bt) < kCfStampSteps)      \
+      P.stamps[(size_t)(bt) * kCfStampSlots + 8 + 4 * (threadIdx.x >> 6) + (i)] =             \
+          (long long)__builtin_amdgcn_s_memtime();                                           \
+  } while (0)
+#define CF_EXP(bit) ((P.exp & (bit)) != 0)
+#else
+#define CF_WSTAMP(bt, i) do {} while (0)
+#define CF_EXP(bit) false
+#endif
+
 // Sum of A[:, a]·B[:, b] over `rows` for every (a, b) < r², one wave per entry (wave sums).
 __device__ void cf_gram(const double* A, const double* B, int rows, int r, double* out) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -253,6 +268,63 @@ __global__ __launch_bounds__(256) void cf_move_kernel(CfParams P, const CfChain*
   }
 }
 
+// Lazy move's row-major working copy: column-major M (rows × R, the session's layout) -> Mr
+// (row r at Mr[r·R .. r·R + R−1]) through an LDS tile of TR rows; eight loads per thread in
+// flight.  Every thread of the block calls it (block barriers inside).
+template <int R>
+__device__ void cf_rows_in(const double* M, double* Mr, int rows, double* tile, int TR) {
+  const int tid = threadIdx.x;
+  for (int r0 = 0; r0 < rows; r0 += TR) {
+    const int nr = min(TR, rows - r0), ne = nr * R;
+    for (int o0 = tid; o0 < ne; o0 += 8 * kCfNT) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int o = min(o0 + u * kCfNT, ne - 1), l = o / nr, rr = o - l * nr;
+        v[u] = gptr(M)[r0 + rr + (size_t)rows * l];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int o = o0 + u * kCfNT, l = o / nr, rr = o - l * nr;
+        if (o < ne) tile[rr * R + l] = v[u];
+      }
+    }
+    __syncthreads();
+    for (int o = tid; o < ne; o += kCfNT) gptr_w(Mr)[(size_t)r0 * R + o] = tile[o];
+    __syncthreads();
+  }
+}
+
+// ... and back at the launch's end: row r of M = (its value as of step cur[r]) · c^(nb − cur[r]),
+// the feature rows (r >= base) from Fl, the others from Mr.
+template <int R>
+__device__ void cf_rows_out(const double* Mr, double* M, int rows, int base, const double* Fl,
+                            const int* cur, const double* cpow, int nb, double* tile, int TR) {
+  const int tid = threadIdx.x;
+  for (int r0 = 0; r0 < rows; r0 += TR) {
+    const int nr = min(TR, rows - r0), ne = nr * R;
+    for (int o0 = tid; o0 < ne; o0 += 8 * kCfNT) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int o = min(o0 + u * kCfNT, ne - 1), row = r0 + o / R;
+        v[u] = row >= base ? Fl[(row - base) * R + o % R] : gptr(Mr)[(size_t)r0 * R + o];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int o = o0 + u * kCfNT;
+        if (o < ne) tile[o] = v[u] * cpow[nb - cur[r0 + o / R]];
+      }
+    }
+    __syncthreads();
+    for (int o = tid; o < ne; o += kCfNT) {
+      const int l = o / nr, rr = o - l * nr;
+      gptr_w(M)[r0 + rr + (size_t)rows * l] = tile[rr * R + l];
+    }
+    __syncthreads();
+  }
+}
+
 // Byte offset of the lazy move's tables (cpow, cur) in the epoch kernel's LDS: past the batch
 // carve of the masks path (w, wn, sU, sV, tU, tV, er, umk, vmk, us, ms, unx, vnx, fcnt, flist).
 GPT_HD size_t cf_lazy_offset(int r, int m, int nfeat) {
@@ -343,6 +415,13 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       const int fo = o / R, l = o - fo * R, side = fo >= P.D1 ? 1 : 0, f = fo - side * P.D1;
       Fl[o] = gptr(side ? C.V : C.U)[(side ? P.n2 : P.n1) + f + (size_t)(side ? P.rowsV : P.rowsU) * l];
     }
+    // Row-major working copies of U and V for the launch, in the gradient buffers (the lazy move
+    // has none): a rating's r entries are then one contiguous run for the sums phase's gathers and
+    // the moves' stores, where the session's column-major layout spreads them over r cache lines.
+    // Transposed through the batch buffers, which are free until the first batch.
+    const int TR = (int)((cf_lazy_offset(R, m, nfeat) - 16 * (size_t)R * R) / (8 * R));
+    cf_rows_in<R>(C.U, C.GU, P.rowsU, sU, TR);
+    cf_rows_in<R>(C.V, C.GV, P.rowsV, sU, TR);
   }
   // lazy path: the next batch's (user, movie, rating) of thread tid < m are loaded during this
   // step's gradient phase and their feature masks after it, so the batch and mask phases of the
@@ -472,26 +551,42 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     if (lazy) {
       // the rating's own row from memory (as of this step), its feature rows from Fc, added in
       // ascending order from 0 as the masks path below does
+      // four items per thread and pass: every item's row load, decay and first three feature
+      // values are read before any sum (a user carries 3 features, 97 % of the rated movies 1-3;
+      // the rest, if any, after)
       for (int o0 = tid; o0 < 2 * B * R; o0 += 4 * kCfNT) {
-        double mv[4];
+        double mv[4], cp[4], fv[4][3];
+        uint64_t rest[4];
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4) {
           const int o = min(o0 + k4 * kCfNT, 2 * B * R - 1);
           const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
           const int id = side ? ms[ii] : us[ii];
-          mv[k4] = gptr(side ? C.V : C.U)[id + (size_t)(side ? P.rowsV : P.rowsU) * l];
+          mv[k4] = gptr(side ? C.GV : C.GU)[(size_t)id * R + l];     // row-major copy
+          cp[k4] = cpow[jl - cur[(side ? P.rowsU : 0) + id]];
+          const double* Fs = Fc + (side ? P.D1 * R : 0) + l;
+          uint64_t mk = (side ? vmk : umk)[ii];
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const bool h = mk != 0;
+            const double xf = Fs[(h ? __ffsll((long long)mk) - 1 : 0) * R];
+            fv[k4][u] = h ? xf : 0.0;                   // + 0.0: the sum is unchanged
+            mk &= mk - 1;
+          }
+          rest[k4] = mk;
         }
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4) {
           const int o = o0 + k4 * kCfNT;
           if (o >= 2 * B * R) break;
           const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
-          const int id = side ? ms[ii] : us[ii];
-          const double mcur = mv[k4] * cpow[jl - cur[(side ? P.rowsU : 0) + id]];
+          const double mcur = mv[k4] * cp[k4];
           mcl[o] = mcur;                                 // o = (side·B + ii)·R + l
-          const double* Fs = Fc + (side ? P.D1 * R : 0) + l;
-          uint64_t mk = (side ? vmk : umk)[ii];
           double f = 0.0;
+#pragma unroll
+          for (int u = 0; u < 3; ++u) f += fv[k4][u];
+          uint64_t mk = rest[k4];
+          const double* Fs = Fc + (side ? P.D1 * R : 0) + l;
           while (mk) {
             const int fb = __ffsll((long long)mk) - 1;
             mk &= mk - 1;
@@ -560,6 +655,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         (side ? sV : sU)[ii * R + l] = gptr(M)[id + (size_t)rows * l] + (side ? P.c : P.b) * f;
       }
     }
+    CF_WSTAMP(bt, 0);
     if (masks && !lazy)
       for (int o = tid; o < P.D1 + P.D2; o += kCfNT) {
         const int side = o >= P.D1 ? 1 : 0, f = o - side * P.D1;
@@ -596,17 +692,27 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         pd4 acc[NTc];
 #pragma unroll
         for (int nt = 0; nt < NTc; ++nt) acc[nt] = pd4{0.0, 0.0, 0.0, 0.0};
+        // every operand read before the first MFMA (KS·(1 + NTc) reads in flight; the scheduling
+        // barrier keeps the compiler from pairing each MFMA with a read and its wait)
+        constexpr int KS = (R + 3) / 4;
+        double av[KS], bv[KS][NTc];
 #pragma unroll
-        for (int k0 = 0; k0 < R; k0 += 4) {
-          const int k = k0 + kl, kc = min(k, R - 1);
-          const double a = k < R ? S[arow * R + kc] : 0.0;
+        for (int ks = 0; ks < KS; ++ks) {
+          const int k = 4 * ks + kl, kc = min(k, R - 1);
+          const double x = S[arow * R + kc];            // unconditional read, then a select
+          av[ks] = k < R ? x : 0.0;
 #pragma unroll
           for (int nt = 0; nt < NTc; ++nt) {
             const int n = min(nt * 16 + rl, R - 1);
-            const double bv = side ? wz[n + R * kc] : wz[kc + R * n];
-            acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[nt], 0, 0, 0);
+            bv[ks][nt] = side ? wz[n + R * kc] : wz[kc + R * n];
           }
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+          for (int nt = 0; nt < NTc; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], bv[ks][nt], acc[nt], 0, 0, 0);
         double* Tt = side ? tV : tU;
 #pragma unroll
         for (int nt = 0; nt < NTc; ++nt)
@@ -639,7 +745,8 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     // 16 × 16 tile of w, K = the batch's ratings in steps of 4 (past B: zero); then the w step of
     // :479-483 per entry.  (The round-4 form summed er·(sumU·sumV)·is2 rating by rating per entry:
     // the same sum, rounded differently.)
-    if (!P.fixw) {
+    if (CF_EXP(2)) __builtin_amdgcn_s_setprio(2);
+    if (!P.fixw && !CF_EXP(8)) {
       constexpr int NTw = (R + 15) / 16;
       const int lane = tid & 63, wv = uni(tid >> 6), rl = lane & 15, kl = lane >> 4;
       for (int t = wv; t < NTw * NTw; t += kCfNW) {
@@ -651,12 +758,28 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         const double* sVz = sV + zo;
         const double* erz = er + zo;
         pd4 acc = pd4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int k0 = 0; k0 < B; k0 += 4) {
-          const int k = k0 + kl, kc = min(k, B - 1);
-          const double a = k < B ? sUz[kc * R + ia] : 0.0;
-          const double bv = erz[kc] * sVz[kc * R + jb];
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
+        // four K steps per pass, every LDS read of the pass issued before its MFMAs (reads
+        // unconditional at clamped rows, the operand past B selected to zero: no branch around
+        // a read, which had left each step's read latency in front of its MFMA)
+        for (int k0 = 0; k0 < B; k0 += 16) {
+          double x4[4], er4[4], s4[4], av[4], bv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int kc = min(k0 + 4 * u + kl, B - 1);
+            x4[u] = sUz[kc * R + ia];
+            er4[u] = erz[kc];
+            s4[u] = sVz[kc * R + jb];
+          }
+          __builtin_amdgcn_sched_barrier(0);             // reads, operands, MFMAs in that order
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            av[u] = k0 + 4 * u + kl < B ? x4[u] : 0.0;
+            bv[u] = er4[u] * s4[u];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -674,34 +797,19 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     } else {
       for (int o = tid; o < R * R; o += kCfNT) wn_l[o] = w_l[o];
     }
-    // gradient rows in rating order (:467-471): the first rating of a user / movie in the batch
-    // sums its row; feature rows sum over the ratings whose user / movie carries them
-    // (the same-id positions of a first occurrence are walked through the next links, ascending)
-    for (int o = tid; o < 2 * B * R; o += kCfNT) {
-      const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
-      const int* nxl = side ? vnx : unx;
-      if (!(nxl[ii] >> 16)) continue;
-      const int id = (side ? ms : us)[ii];
-      const double* T = side ? tU : tV;     // Vtemp = e·(sumU*w), Utemp = e·(sumV*w')
-      double g = 0.0;
-      for (int z = ii; z >= 0; z = (nxl[z] & 0xFFFF) - 1) g += P.a * (er[z] * T[z * R + l]) * is2;
-      const size_t e = id + (size_t)(side ? P.rowsV : P.rowsU) * l;
-      if (lazy) {                                     // the row's move of this step (cf_move)
-        double* M = side ? C.V : C.U;
-        const double m0 = mcl[o];                     // the value the sums phase read (no update since)
-        gptr_w(M)[e] = m0 + P.epsU * (g * cN - m0 / su2) / 2;
-      } else {
-        gptr_w(side ? C.GV : C.GU)[e] = g * cN;
-      }
-    }
-    if (lazy) {
+    CF_WSTAMP(bt, 1);
+    if (lazy && !CF_EXP(4)) {
       // feature rows: G[f, l] = Σ_ii [f ∈ mask_ii]·er_ii·T[ii, l] on the fp64 matrix cores (one
       // wave per 16 features × 16 columns of a side, K = the ratings; A = the mask bit as 0 / 1),
-      // then the move of every feature the batch carries, in LDS (Fl)
+      // then the move of every feature the batch carries, in LDS (Fl).  Before the gradient rows:
+      // the tiles' MFMA chains then overlap the rows' VALU / LDS work of the other waves of each
+      // SIMD (after them, the tiles of two waves per SIMD ran alone at the end of the phase)
       constexpr int LT = (R + 15) / 16;
       const int lane = tid & 63, wv = uni(tid >> 6), rl = lane & 15, kl = lane >> 4;
       const int FT1 = (P.D1 + 15) / 16, FT2 = (P.D2 + 15) / 16;
       // tiles from the last wave down, so they do not queue behind gradw's tiles on waves 0, 1, ..
+      // (one tile per wave: all LT column tiles of 16 features on one wave, their chains
+      // interleaved, measured slower — 15.8-17.1 k against 10.9-15.6 k cycles)
       for (int t = kCfNW - 1 - wv; t < (FT1 + FT2) * LT; t += kCfNW) {
         const int ft = t / LT, lt = t - ft * LT, side = ft >= FT1 ? 1 : 0;
         const int f0 = (ft - side * FT1) * 16, Ds = side ? P.D2 : P.D1;
@@ -712,12 +820,31 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         const double* erz = er + zo;
         const int fa = f0 + rl, lb = min(lt * 16 + rl, R - 1);
         pd4 acc = pd4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int k0 = 0; k0 < B; k0 += 4) {
-          const int k = k0 + kl, kc = min(k, B - 1);
-          const double a = (k < B && ((mk[kc] >> fa) & 1ull)) ? 1.0 : 0.0;
-          const double bv = erz[kc] * T[kc * R + lb];
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
+        for (int k0 = 0; k0 < B; k0 += 16) {            // (four K steps per pass, as gradw's)
+          // the pass's twelve reads issued together, then the operands, then the MFMAs (the
+          // scheduling barriers keep the compiler from interleaving them one step at a time)
+          uint64_t mr[4];
+          double er4[4], t4[4], av[4], bv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int kc = min(k0 + 4 * u + kl, B - 1);
+            mr[u] = mk[kc];
+            er4[u] = erz[kc];
+            t4[u] = T[kc * R + lb];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            // the bit as arithmetic, no select: a select let the compiler sink the mask read
+            // under a branch
+            const unsigned bit = (unsigned)(mr[u] >> fa) & 1u & (unsigned)(k0 + 4 * u + kl < B);
+            av[u] = (double)bit;
+            bv[u] = er4[u] * t4[u];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
         }
         const double ab = P.a * (side ? P.c : P.b);
         const unsigned long long hs = hit[side];
@@ -732,6 +859,50 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         }
       }
     }
+    CF_WSTAMP(bt, 2);
+    if (CF_EXP(2)) __builtin_amdgcn_s_setprio(0);
+    // gradient rows in rating order (:467-471): the first rating of a user / movie in the batch
+    // sums its row; feature rows sum over the ratings whose user / movie carries them
+    // (the same-id positions of a first occurrence are walked through the next links, ascending)
+    // Four items per thread and pass: every item's link word, id, first term and (lazy) row value
+    // read before any of them is summed; the rest of a walk (an id seen twice or more in the
+    // batch) after.
+    for (int o0 = tid; o0 < (CF_EXP(1) ? 0 : 2 * B * R); o0 += 4 * kCfNT) {
+      int nv[4], idv[4];
+      double t0[4], m0v[4];
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const int o = min(o0 + k4 * kCfNT, 2 * B * R - 1);
+        const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+        nv[k4] = (side ? vnx : unx)[ii];
+        idv[k4] = (side ? ms : us)[ii];
+        const double* T = side ? tU : tV;   // Vtemp = e·(sumU*w), Utemp = e·(sumV*w')
+        t0[k4] = er[ii] * T[ii * R + l];
+        if constexpr (lazy) m0v[k4] = mcl[o];  // the value the sums phase read (no update since)
+        else m0v[k4] = 0.0;
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const int o = o0 + k4 * kCfNT;
+        if (o >= 2 * B * R) break;
+        if (!(nv[k4] >> 16)) continue;
+        const int side = o / (B * R), x = o - side * (B * R), l = x - (x / R) * R;
+        const int* nxl = side ? vnx : unx;
+        const double* T = side ? tU : tV;
+        double g = 0.0;
+        g += P.a * t0[k4] * is2;
+        for (int z = (nv[k4] & 0xFFFF) - 1; z >= 0; z = (nxl[z] & 0xFFFF) - 1)
+          g += P.a * (er[z] * T[z * R + l]) * is2;
+        const int id = idv[k4];
+        if (lazy) {                                   // the row's move of this step (cf_move)
+          const double m0 = m0v[k4];
+          gptr_w(side ? C.GV : C.GU)[(size_t)id * R + l] = m0 + P.epsU * (g * cN - m0 / su2) / 2;
+        } else {
+          gptr_w(side ? C.GV : C.GU)[id + (size_t)(side ? P.rowsV : P.rowsU) * l] = g * cN;
+        }
+      }
+    }
+    CF_WSTAMP(bt, 3);
     for (int o = tid; o < (lazy ? 0 : (P.D1 + P.D2) * R); o += kCfNT) {
       const int side = o >= P.D1 * R ? 1 : 0;
       const int x = side ? o - P.D1 * R : o, f = x / R, l = x - f * R;
@@ -799,16 +970,9 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     if (lazy) lds_barrier(); else __syncthreads();    // (no global writes since the last fence)
   }
   if (lazy) {                                         // every row brought to the launch's end
-    const int nUe = P.rowsU * R;
-    for (int o = tid; o < nUe + P.rowsV * R; o += kCfNT) {
-      const int side = o >= nUe ? 1 : 0, x = o - side * nUe;
-      const int rows = side ? P.rowsV : P.rowsU, l = x / rows, row = x - l * rows;
-      const int d = nb - cur[(side ? P.rowsU : 0) + row];
-      double* M = side ? C.V : C.U;
-      const int base = side ? P.n2 : P.n1;
-      if (row >= base) gptr_w(M)[x] = Fl[((side ? P.D1 : 0) + row - base) * R + l] * cpow[d];
-      else if (d > 0) gptr_w(M)[x] = gptr(M)[x] * cpow[d];
-    }
+    const int TR = (int)((cf_lazy_offset(R, m, nfeat) - 16 * (size_t)R * R) / (8 * R));
+    cf_rows_out<R>(C.GU, C.U, P.rowsU, P.n1, Fl, cur, cpow, nb, sU, TR);
+    cf_rows_out<R>(C.GV, C.V, P.rowsV, P.n2, Fl + P.D1 * R, cur + P.rowsU, cpow, nb, sU, TR);
   }
   for (int o = tid; o < R * R; o += kCfNT) C.w[o] = w_l[o];
 }

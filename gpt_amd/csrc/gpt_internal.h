@@ -241,8 +241,13 @@ struct CfParams {
   const uint64_t* umask;   // n1: bitmask of each user's feature rows (D1 <= 64), else null
   const uint64_t* vmask;   // n2
   long long* stamps;     // diagnostics: kCfStampSteps x kCfStampSlots s_memtime of chain 0, or null
+  int exp;               // diagnostic builds only (CF_WSTAMPS): timing experiments, GPTSGLD_CF_EXP
 };
-constexpr int kCfStampSteps = 64, kCfStampSlots = 8;
+// CF_WSTAMPS (diagnostic builds, make diag): 4 more stamps per wave of the 16 (cf.hip CF_WSTAMP)
+#ifndef CF_WSTAMPS
+#define CF_WSTAMPS 0
+#endif
+constexpr int kCfStampSteps = 64, kCfStampSlots = CF_WSTAMPS ? 8 + 4 * 16 : 8;
 
 struct CfChain {
   const int32_t* tr_user;   // N   0-based ids

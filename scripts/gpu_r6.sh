@@ -36,6 +36,9 @@ for s in "$@"; do
     ref)      run ref 400 python -u bench.py --workload kin40k_ref --no-cpu-baseline ;;
     profref)  run profref 500 $RP -d gpurun_out/${T}_prof_ref -o run -- python -u bench.py --workload kin40k_ref --no-cpu-baseline --no-single-chain; squeeze ref ;;
     ml)       run ml 400 python -u bench.py --workload movielens ;;
+    mltests)  run mltests 300 $PYT tests/test_gpu_movielens.py ;;
+    mlstamps) run mlstamps 300 python -u scripts/ml_stamps.py ;;
+    mlwstamps) run mlwstamps 300 env GPTSGLD_LIB=gpt_amd/libgptsgld_diag.so python -u scripts/ml_stamps.py ;;
     mlnocpu)  run mlnocpu 300 python -u bench.py --workload movielens --no-cpu-baseline ;;
     pp)       run pp 400 python -u bench.py --workload powerplant --no-cpu-baseline ;;
     timeline) run timeline 300 env GPTSGLD_LIB=gpt_amd/libgptsgld_tl.so python -u scripts/timeline.py --out gpurun_out/${T}_timeline.json ;;
