@@ -864,42 +864,22 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     // gradient rows in rating order (:467-471): the first rating of a user / movie in the batch
     // sums its row; feature rows sum over the ratings whose user / movie carries them
     // (the same-id positions of a first occurrence are walked through the next links, ascending)
-    // Four items per thread and pass: every item's link word, id, first term and (lazy) row value
-    // read before any of them is summed; the rest of a walk (an id seen twice or more in the
-    // batch) after.
-    for (int o0 = tid; o0 < (CF_EXP(1) ? 0 : 2 * B * R); o0 += 4 * kCfNT) {
-      int nv[4], idv[4];
-      double t0[4], m0v[4];
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const int o = min(o0 + k4 * kCfNT, 2 * B * R - 1);
-        const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
-        nv[k4] = (side ? vnx : unx)[ii];
-        idv[k4] = (side ? ms : us)[ii];
-        const double* T = side ? tU : tV;   // Vtemp = e·(sumU*w), Utemp = e·(sumV*w')
-        t0[k4] = er[ii] * T[ii * R + l];
-        if constexpr (lazy) m0v[k4] = mcl[o];  // the value the sums phase read (no update since)
-        else m0v[k4] = 0.0;
-      }
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const int o = o0 + k4 * kCfNT;
-        if (o >= 2 * B * R) break;
-        if (!(nv[k4] >> 16)) continue;
-        const int side = o / (B * R), x = o - side * (B * R), l = x - (x / R) * R;
-        const int* nxl = side ? vnx : unx;
-        const double* T = side ? tU : tV;
-        double g = 0.0;
-        g += P.a * t0[k4] * is2;
-        for (int z = (nv[k4] & 0xFFFF) - 1; z >= 0; z = (nxl[z] & 0xFFFF) - 1)
-          g += P.a * (er[z] * T[z * R + l]) * is2;
-        const int id = idv[k4];
-        if (lazy) {                                   // the row's move of this step (cf_move)
-          const double m0 = m0v[k4];
-          gptr_w(side ? C.GV : C.GU)[(size_t)id * R + l] = m0 + P.epsU * (g * cN - m0 / su2) / 2;
-        } else {
-          gptr_w(side ? C.GV : C.GU)[id + (size_t)(side ? P.rowsV : P.rowsU) * l] = g * cN;
-        }
+    // (four items per thread with their reads batched measured slower: 260.5-261.3 k against
+    // 268.3-268.5 k fold-steps/s, profiles/r6_ml_ab.txt)
+    for (int o = tid; o < (CF_EXP(1) ? 0 : 2 * B * R); o += kCfNT) {
+      const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+      const int* nxl = side ? vnx : unx;
+      if (!(nxl[ii] >> 16)) continue;
+      const int id = (side ? ms : us)[ii];
+      const double* T = side ? tU : tV;     // Vtemp = e·(sumU*w), Utemp = e·(sumV*w')
+      double g = 0.0;
+      for (int z = ii; z >= 0; z = (nxl[z] & 0xFFFF) - 1) g += P.a * (er[z] * T[z * R + l]) * is2;
+      const size_t e = id + (size_t)(side ? P.rowsV : P.rowsU) * l;
+      if (lazy) {                                     // the row's move of this step (cf_move)
+        const double m0 = mcl[o];                     // the value the sums phase read (no update since)
+        gptr_w(side ? C.GV : C.GU)[(size_t)id * R + l] = m0 + P.epsU * (g * cN - m0 / su2) / 2;
+      } else {
+        gptr_w(side ? C.GV : C.GU)[e] = g * cN;
       }
     }
     CF_WSTAMP(bt, 3);

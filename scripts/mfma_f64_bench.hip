@@ -31,6 +31,48 @@ __global__ void bench(long long* out, double* sink, int nit) {
   sink[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// v_mfma_f64_4x4x4f64 (four 4 × 4 blocks, K = 4, one double per lane in and out)
+template <int C>
+__global__ void bench4(long long* out, double* sink, int nit) {
+  const int lane = threadIdx.x & 63;
+  double a = 1.0 + lane * 1e-9, b = 1.0 - lane * 1e-9;
+  double acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = (double)c;
+  __syncthreads();
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < nit; ++i) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, acc[c], 0, 0, 0);
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) s += acc[c];
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)] = t1 - t0;
+  sink[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <int C>
+static void run4(int W, int nit) {
+  const int nb = 256;
+  long long* d_out;
+  double* d_sink;
+  (void)hipMalloc(&d_out, sizeof(long long) * nb * W);
+  (void)hipMalloc(&d_sink, sizeof(double) * nb * W * 64);
+  for (int rep = 0; rep < 2; ++rep)
+    hipLaunchKernelGGL(bench4<C>, dim3(nb), dim3(64 * W), 0, 0, d_out, d_sink, nit);
+  (void)hipDeviceSynchronize();
+  std::vector<long long> h(nb * W);
+  (void)hipMemcpy(h.data(), d_out, sizeof(long long) * nb * W, hipMemcpyDeviceToHost);
+  std::sort(h.begin(), h.end());
+  const double per_wave = (double)h[h.size() / 2] / ((double)nit * C);
+  printf("4x4x4 f64: waves/WG %2d chains %d : %.1f cycles per MFMA of a wave, %.1f per MFMA per SIMD\n",
+         W, C, per_wave, per_wave / std::max(1, W / 4));
+  (void)hipFree(d_out);
+  (void)hipFree(d_sink);
+}
+
 // The MovieLens feature-tile pass: 12 LDS reads, one wait, 8 VALU operand ops, 4 chained MFMAs
 // whose sources the next pass's reads and VALU overwrite (PP = 1), or the same with the next
 // pass's reads issued before this pass's MFMAs into a second register set (PP = 2).
@@ -150,6 +192,10 @@ int main() {
     run<1>(W, nit);
     run<2>(W, nit);
     run<4>(W, nit);
+  }
+  for (int W : {1, 4, 16}) {
+    run4<1>(W, nit);
+    run4<4>(W, nit);
   }
   for (int W : {1, 4, 8, 16}) {
     run_pass<1>(W, 64);
