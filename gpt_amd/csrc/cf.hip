@@ -560,7 +560,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4) {
           const int o = min(o0 + k4 * kCfNT, 2 * B * R - 1);
-          const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+          const int side = o >= B * R ? 1 : 0, x = o - side * (B * R), ii = x / R, l = x - ii * R;
           const int id = side ? ms[ii] : us[ii];
           mv[k4] = gptr(side ? C.GV : C.GU)[(size_t)id * R + l];     // row-major copy
           cp[k4] = cpow[jl - cur[(side ? P.rowsU : 0) + id]];
@@ -579,7 +579,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         for (int k4 = 0; k4 < 4; ++k4) {
           const int o = o0 + k4 * kCfNT;
           if (o >= 2 * B * R) break;
-          const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+          const int side = o >= B * R ? 1 : 0, x = o - side * (B * R), ii = x / R, l = x - ii * R;
           const double mcur = mv[k4] * cp[k4];
           mcl[o] = mcur;                                 // o = (side·B + ii)·R + l
           double f = 0.0;
@@ -605,7 +605,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
           const int o = o0 + k4 * kCfNT;
           ok[k4] = o < 2 * B * R;
           const int oc = ok[k4] ? o : o0;
-          const int side = oc / (B * R), x = oc - side * (B * R), ii = x / R, l = x - ii * R;
+          const int side = oc >= B * R ? 1 : 0, x = oc - side * (B * R), ii = x / R, l = x - ii * R;
           const double* M = side ? C.V : C.U;
           const int rows = side ? P.rowsV : P.rowsU;
           const int id = side ? ms[ii] : us[ii];
@@ -625,7 +625,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         for (int k4 = 0; k4 < 4; ++k4) {
           if (!ok[k4]) continue;
           const int o = o0 + k4 * kCfNT;
-          const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+          const int side = o >= B * R ? 1 : 0, x = o - side * (B * R), ii = x / R, l = x - ii * R;
           const double* M = side ? C.V : C.U;
           const int rows = side ? P.rowsV : P.rowsU;
           const int base = side ? P.n2 : P.n1;
@@ -644,7 +644,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
       }
     } else {
       for (int o = tid; o < 2 * B * R; o += kCfNT) {
-        const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+        const int side = o >= B * R ? 1 : 0, x = o - side * (B * R), ii = x / R, l = x - ii * R;
         const double* M = side ? C.V : C.U;
         const int rows = side ? P.rowsV : P.rowsU;
         const int id = side ? ms[ii] : us[ii];
@@ -867,7 +867,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     // (four items per thread with their reads batched measured slower: 260.5-261.3 k against
     // 268.3-268.5 k fold-steps/s, profiles/r6_ml_ab.txt)
     for (int o = tid; o < (CF_EXP(1) ? 0 : 2 * B * R); o += kCfNT) {
-      const int side = o / (B * R), x = o - side * (B * R), ii = x / R, l = x - ii * R;
+      const int side = o >= B * R ? 1 : 0, x = o - side * (B * R), ii = x / R, l = x - ii * R;
       const int* nxl = side ? vnx : unx;
       if (!(nxl[ii] >> 16)) continue;
       const int id = (side ? ms : us)[ii];
