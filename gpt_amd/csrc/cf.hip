@@ -268,6 +268,34 @@ __global__ __launch_bounds__(256) void cf_move_kernel(CfParams P, const CfChain*
   }
 }
 
+// The value of lane λ ^ j (j < 64, a power of two) without an LDS round trip: DPP within rows
+// (quad_perm for 1, 2; row_ror 4 / 12 picked per lane for 4; row_ror 8), v_permlane16/32_swap
+// across rows.  Which rotation / swap slot holds the partner is read off the lane ids themselves
+// (XorSel, formed once).
+struct XorSel { bool r4, s16, s32; };
+__device__ __forceinline__ XorSel xor_sel(int lane) {
+  XorSel x;
+  x.r4 = __builtin_amdgcn_mov_dpp(lane, 0x124, 0xF, 0xF, false) == (lane ^ 4);
+  x.s16 = (int)__builtin_amdgcn_permlane16_swap((unsigned)lane, (unsigned)lane, false, false)[0] ==
+          (lane ^ 16);
+  x.s32 = (int)__builtin_amdgcn_permlane32_swap((unsigned)lane, (unsigned)lane, false, false)[0] ==
+          (lane ^ 32);
+  return x;
+}
+__device__ __forceinline__ int xor_lane(int v, int j, const XorSel& x) {
+  if (j == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);      // quad_perm 1,0,3,2
+  if (j == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);      // quad_perm 2,3,0,1
+  if (j == 8) return __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);     // row_ror 8
+  if (j == 4) {
+    const int a = __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);         // row_ror 4
+    const int b = __builtin_amdgcn_mov_dpp(v, 0x12C, 0xF, 0xF, false);         // row_ror 12
+    return x.r4 ? a : b;
+  }
+  const auto sw = j == 16 ? __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false)
+                          : __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+  return (int)((j == 16 ? x.s16 : x.s32) ? sw[0] : sw[1]);
+}
+
 // Lazy move's row-major working copy: column-major M (rows × R, the session's layout) -> Mr
 // (row r at Mr[r·R .. r·R + R−1]) through an LDS tile of TR rows; eight loads per thread in
 // flight.  Every thread of the block calls it (block barriers inside).
@@ -458,7 +486,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
     // per (side, ii): the feature bitmask, the first-occurrence flag and the next occurrence
     if (B <= 128) {
       // the links by sorting: wave `side` sorts the 128 keys (id << 8 | position) of its side
-      // (two per lane, bitonic, lane exchanges by __shfl_xor), so equal ids end up adjacent in
+      // (two per lane, bitonic, lane exchanges by DPP / permlane), so equal ids end up adjacent in
       // ascending position: a key's successor with the same id is its next occurrence, and a key
       // whose predecessor differs is the first (the round-4 form compared every pair, 11.6 k
       // cycles of the step); the masks go to LDS from the other waves
@@ -467,6 +495,7 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
         const int* ids = wv ? ms : us;
         int k0 = lane < B ? (ids[lane] << 8) | lane : 0x7fffffff;
         int k1 = lane + 64 < B ? (ids[lane + 64] << 8) | (lane + 64) : 0x7fffffff;
+        const XorSel xs = xor_sel(lane);
 #pragma unroll
         for (int k = 2; k <= 128; k <<= 1) {
 #pragma unroll
@@ -476,7 +505,9 @@ __global__ __launch_bounds__(kCfNT) void cf_epoch_kernel(CfParams P, const CfCha
               k0 = lo;
               k1 = hi;
             } else {
-              const int o0 = __shfl_xor(k0, j), o1 = __shfl_xor(k1, j);
+              // (DPP / permlane exchanges: __shfl_xor's ds_bpermute round trips made the 28
+              // stages a 4.4 k-cycle latency chain)
+              const int o0 = xor_lane(k0, j, xs), o1 = xor_lane(k1, j, xs);
               const bool low = (lane & j) == 0;        // this element is the lower of its pair
               const bool asc0 = (lane & k) == 0, asc1 = ((lane + 64) & k) == 0;
               k0 = (low == asc0) ? min(k0, o0) : max(k0, o0);
