@@ -91,6 +91,21 @@ __device__ __forceinline__ double group8_sum(double v) {
   return v + dpp_partner<4>(v);     // row_half_mirror pairs the two quads of the group
 }
 
+// floor(x / d) for a divisor fixed over a loop: one v_mul_hi_u32 (and a select for d = 1)
+// instead of the ~30 VALU instructions of a runtime integer division.  M = ⌈2³²/d⌉ =
+// ⌊(2³² − 1)/d⌋ + 1 (one 32-bit division where the divisor is formed); exact whenever
+// x·d ≤ 2³²: with x = qd + r, x·M/2³² = q + r/d + x·δ/(d·2³²), δ = M·d − 2³² < d, so the
+// fraction stays below 1.  (d = 1 would need M = 2³²: m = 0 marks it.)
+struct FastDiv {
+  uint32_t m;
+};
+__device__ __forceinline__ FastDiv fast_div(int d) {
+  return FastDiv{d == 1 ? 0u : 0xFFFFFFFFu / (uint32_t)d + 1u};
+}
+__device__ __forceinline__ int fdiv(int x, FastDiv f) {
+  return f.m ? (int)__umulhi((uint32_t)x, f.m) : x;
+}
+
 // 1/x from the hardware reciprocal plus two Newton steps (within 1 ulp; 5 VALU ops instead of
 // the ~10 of an IEEE division).
 __device__ __forceinline__ double rcp_nr(double x) {

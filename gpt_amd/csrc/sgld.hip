@@ -86,6 +86,9 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   const int B1 = has_next ? min(m, P.N - s1) : 0;
   const int32_t* ord1 = C.order + (size_t)((has_next ? e1 : e) & 1) * P.N + (has_next ? s1 : start);
   const int Bs = Bt, Bsn = B1;         // this workgroup's batch columns and next-batch columns
+  // the element loops' divisors (fast_div: no runtime integer division per element)
+  const FastDiv fdMP = fast_div(MP), fdNP = fast_div(NP), fdBs = fast_div(Bs), fdn = fast_div(n),
+                fdNQ = fast_div(64 * unoise_nq(n));
   // rows of the next batch this lane touches into L2 during the V-phase (P5 streams them at the
   // end of the step): lanes 0-31 / 32-63 of wave w cover rows 2(w + kNW·x) + {0, 1}
   int trow[kTouch];
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   {
     const double* tsrc = C.temp + (size_t)(t & 1) * D * R * m;
     for (int o = tid; o < D * R * MP; o += kNT) {   // zero tail: unrolled reads run past Bs
-      const int row = o / MP, i = o - row * MP;
+      const int row = fdiv(o, fdMP), i = o - row * MP;
       temp_l[o] = i < Bs ? gptr(tsrc)[row * m + i] : 0.0;
     }
     for (int i = tid; i < MP; i += kNT) res_l[i] = 0.0;
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   }
   // coef[l][i] = A[l][i]·res[i]; stage U^(k) (the union slot of temp_l is free now)
   for (int o = tid; o < R * Bs; o += kNT) {
-    const int l = o / Bs, i = o - l * Bs;
+    const int l = fdiv(o, fdBs), i = o - l * Bs;
     coef_l[l * MP + i] *= res_l[i];
   }
   const double* Ug = C.U + (size_t)n * R * k;
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   // spread over the threads here, so P2's thread-per-row drive reads its ξ[j, :] from LDS
   const bool noise0 = (P.langevin || P.ncls) && !P.rms;
   for (int o = tid; o < R * NP; o += kNT) {
-    const int l = o / NP, j = o - l * NP;
+    const int l = fdiv(o, fdNP), j = o - l * NP;
     U_l[l * NS + j] = j < n ? gptr(Ug)[j + (size_t)n * l] : 0.0;
     if (j >= n || !noise0) W_l[l * NS + j] = 0.0;
   }
@@ -306,7 +309,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     const uint32_t c3 = P.ncls ? (uint32_t)(k + D * 2 * (blockIdx.y % P.ncls)) : (uint32_t)k;
     const int NQ = unoise_nq(n);
     for (int qd = tid; qd < R * NQ * 64; qd += kNT) {
-      const int l = qd / (NQ * 64), q = (qd >> 6) - l * NQ, lam = qd & 63;
+      const int l = fdiv(qd, fdNQ), q = (qd >> 6) - l * NQ, lam = qd & 63;
       double z[4];
       normal_quad<4>(C.seed, (uint32_t)qd, (uint32_t)t, kUNoise, c3, z);
 #pragma unroll
@@ -386,7 +389,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     sk = sqrt(blk_sum(esum, red) / ((double)n * R));
     const int NQ = unoise_nq(n);
     for (int qd = tid; qd < R * NQ * 64; qd += kNT) {   // drive √εU_k·gradU/2 + ξ (:1231)
-      const int l = qd / (NQ * 64), q = (qd >> 6) - l * NQ, lam = qd & 63;
+      const int l = fdiv(qd, fdNQ), q = (qd >> 6) - l * NQ, lam = qd & 63;
       double z[4];
       normal_quad<4>(C.seed, (uint32_t)qd, (uint32_t)t, kUNoise, (uint32_t)k, z);
 #pragma unroll
@@ -406,13 +409,13 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
   if (pass == 1) {
     // pass 0's U is the "old U" of pass 1 (re-read from HBM when it is not kept in LDS)
     for (int o = tid; o < R * n; o += kNT) {
-      const int l = o / n, j = o - l * n;
+      const int l = fdiv(o, fdn), j = o - l * n;
       gptr_w(C.U + (size_t)n * R * k)[o] = U_l[l * NS + j];
     }
     const uint32_t c3 = (uint32_t)(k + D * (2 * (blockIdx.y % P.ncls) + 1));
     const int NQ = unoise_nq(n);
     for (int qd = tid; qd < R * NQ * 64; qd += kNT) {
-      const int l = qd / (NQ * 64), q = (qd >> 6) - l * NQ, lam = qd & 63;
+      const int l = fdiv(qd, fdNQ), q = (qd >> 6) - l * NQ, lam = qd & 63;
       double z[4] = {0.0, 0.0, 0.0, 0.0};
       if (P.langevin) normal_quad<4>(C.seed, (uint32_t)qd, (uint32_t)t, kUNoise, c3, z);
 #pragma unroll
@@ -593,7 +596,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
       double* nrm = gram + 4 * R * R; // r
       blk_gram<R>(W_l, W_l, NS, n, 2, nrm, red);
       for (int o = tid; o < R * NP; o += kNT) {
-        const int l = o / NP, j = o - l * NP;
+        const int l = fdiv(o, fdNP), j = o - l * NP;
         U_l[l * NS + j] = j < n ? W_l[l * NS + j] / sqrt(nrm[l]) : 0.0;
       }
     }
@@ -607,7 +610,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(GPT_WPE))) 
     double* Uk = C.U + (size_t)n * R * k;
     double* Us = (store && C.U_store) ? C.U_store + ((size_t)slot * D + k) * n * R : nullptr;
     for (int o = tid; o < R * n; o += kNT) {
-      const int l = o / n, j = o - l * n;
+      const int l = fdiv(o, fdn), j = o - l * n;
       const double u = U_l[l * NS + j];
       gptr_w(Uk)[o] = u;
       if (Us) gptr_w(Us)[o] = u;
@@ -654,6 +657,7 @@ __global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
   const int n = P.n, D = P.D, m = P.m;
   const StepLayout L = step_layout(n, D, R, P.Q, m);
   const int NP = L.NP, NS = L.NS;
+  const FastDiv fdNP = fast_div(NP);
   double* U_l = (double*)(smem + L.o_U);
   const int e = (int)(t / P.nb), b = (int)(t - (long long)e * P.nb);
   const int start = b * m;
@@ -661,7 +665,7 @@ __global__ __launch_bounds__(kNT) void temp_init_kernel(StepParams P,
   const int32_t* ord = C.order + (size_t)(e & 1) * P.N + start;
   const double* Uk = C.U + (size_t)n * R * k;
   for (int o = tid; o < R * NP; o += kNT) {
-    const int l = o / NP, j = o - l * NP;
+    const int l = fdiv(o, fdNP), j = o - l * NP;
     U_l[l * NS + j] = j < n ? Uk[j + (size_t)n * l] : 0.0;
   }
   __syncthreads();
