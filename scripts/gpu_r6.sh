@@ -40,6 +40,7 @@ for s in "$@"; do
     mlstamps) run mlstamps 300 python -u scripts/ml_stamps.py ;;
     mlwstamps) run mlwstamps 300 env GPTSGLD_LIB=gpt_amd/libgptsgld_diag.so python -u scripts/ml_stamps.py ;;
     mlab)     for i in 1 2; do run mlab_head$i 300 python -u bench.py --workload movielens --no-cpu-baseline; run mlab_var$i 300 env GPTSGLD_LIB=gpt_amd/libgptsgld_var.so python -u bench.py --workload movielens --no-cpu-baseline; done ;;
+    predab)   run predtests 300 $PYT tests/test_gpu_parity.py -k "pred" ; for i in 1 2; do run predab_head$i 200 python -u scripts/time_pred.py --S 224 --n 150 --r 20 --vphases rows; run predab_var$i 200 env GPTSGLD_LIB=gpt_amd/libgptsgld_var.so python -u scripts/time_pred.py --S 224 --n 150 --r 20 --vphases rows; done ;;
     mlnocpu)  run mlnocpu 300 python -u bench.py --workload movielens --no-cpu-baseline ;;
     pp)       run pp 400 python -u bench.py --workload powerplant --no-cpu-baseline ;;
     timeline) run timeline 300 env GPTSGLD_LIB=gpt_amd/libgptsgld_tl.so python -u scripts/timeline.py --out gpurun_out/${T}_timeline.json ;;
